@@ -1,0 +1,143 @@
+/*
+ * rasr_gmm.h -- C-ABI of the MI355X diagonal-covariance GMM feature scorer.
+ *
+ * This is the drop-in boundary for RASR's acoustic scoring hot path
+ * (Mm::FeatureScorer plugin surface, src/Mm/FeatureScorer.hh:28-164).  Plain
+ * pointers and sizes only; no HIP or torch types.  Every entry point returns
+ * an int status (GMM_OK == 0, negative on error, message via gmm_last_error());
+ * nothing throws across the ABI (the reference is built -fno-exceptions,
+ * config/cc-gcc.make:27).  One handle per GPU; a handle is not thread-safe
+ * (RASR scorers are single-thread objects, src/Core/ReferenceCounting.hh:43-77).
+ *
+ * Score tables are mixture-major: score(e, t) = scores[e * score_stride + t],
+ * the layout of BatchFeatureScorerBase::scores_ (src/Mm/BatchFeatureScorer.hh:177-186).
+ */
+#ifndef RASR_GMM_H
+#define RASR_GMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GMM_OK 0
+#define GMM_ERR_INVALID_ARGUMENT -1
+#define GMM_ERR_UNSUPPORTED -2
+#define GMM_ERR_DEVICE -3
+#define GMM_ERR_OUT_OF_MEMORY -4
+#define GMM_ERR_CAPACITY -5
+
+/* Feature-scorer types; numeric values are Mm::Module_::FeatureScorerType
+ * (src/Mm/Module.hh:48-70), names are the reference's registration strings
+ * (src/Mm/Module.cc:84-107). */
+typedef enum {
+    GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT = 0, /* "batch-diagonal-maximum-float" BatchFeatureScorer.cc:120-234 */
+    GMM_BATCH_DIAGONAL_MAXIMUM_INT   = 3, /* "batch-diagonal-maximum-int"   BatchFeatureScorer.cc:293-474 */
+    GMM_BATCH_DIAGONAL_MAXIMUM_FAST  = 4, /* "batch-diagonal-maximum-fast"  BatchFeatureScorer.cc:537-604 */
+    GMM_DIAGONAL_MAXIMUM             = 5, /* "diagonal-maximum"   GaussDiagonalMaximumFeatureScorer.cc */
+    GMM_SIMD_DIAGONAL_MAXIMUM        = 9  /* "SIMD-diagonal-maximum" SimdFeatureScorer.cc            */
+} gmm_scorer_type;
+
+/* In-memory Mm::MixtureSet (src/Mm/MixtureSet.hh:140-212).  Replaces what the
+ * reference scorers read in init() (SimdFeatureScorer.cc:64-104,
+ * GaussDiagonalMaximumFeatureScorer.cc:64-86, BatchFeatureScorer.cc:59-75).
+ * Densities may be shared between mixtures (CSR over mixture entries). */
+typedef struct {
+    uint32_t        dimension;           /* MixtureSet::dimension()                        */
+    uint32_t        n_means;
+    const float*    means;               /* n_means x dimension (Mean, GaussDensity.hh)     */
+    uint32_t        n_covariances;
+    const float*    variances;           /* n_covariances x dimension: Covariance::diagonal() */
+    uint32_t        n_densities;
+    const uint32_t* density_mean;        /* GaussDensity::meanIndex()       [n_densities]    */
+    const uint32_t* density_covariance;  /* GaussDensity::covarianceIndex() [n_densities]    */
+    uint32_t        n_mixtures;
+    const uint32_t* mixture_offsets;     /* [n_mixtures + 1], entries of mixture m are [o[m], o[m+1]) */
+    const uint32_t* mixture_densities;   /* Mixture::densityIndex(dns)      [n_entries]      */
+    const double*   mixture_log_weights; /* Mixture::logWeight(dns) (Mm::Weight = f64) [n_entries] */
+} gmm_mixture_set;
+
+/* Scorer configuration (Core::Configuration parameters of the replaced scorers). */
+typedef struct {
+    float    mixture_weight_scale; /* "mixture-weight-scale" GaussDiagonalMaximumFeatureScorer.cc:38-40 (default 1) */
+    float    gaussian_scale;       /* "gaussian-scale" GaussDiagonalMaximumFeatureScorer.cc:42-44 (default 1)       */
+    float    score_scale;          /* FeatureScorerScaling scale, ScaledFeatureScorer.hh:62-64 (default 1)         */
+    uint32_t max_frames;           /* largest n_frames of one gmm_score_* call ("buffer-size", cc:28-29)         */
+    uint32_t mixture_begin;        /* mixture shard [begin, end) scored by this handle; 0,0 = all mixtures        */
+    uint32_t mixture_end;
+    uint32_t flags;                /* reserved, 0                                                                 */
+} gmm_scorer_config;
+
+typedef struct gmm_scorer gmm_scorer;
+
+/* Fill *cfg with the reference defaults. */
+void gmm_default_config(gmm_scorer_config* cfg);
+
+/* Prepare the model on the host exactly as the reference scorer's init() does
+ * (quantization scale, 1/sqrt(var), prepared means, constant weights) and
+ * upload it to `device`.  Replaces the FeatureScorerFactory::createInstance
+ * call (src/Mm/FeatureScorerFactory.hh:114-122) for the selected type. */
+int gmm_scorer_create(const gmm_mixture_set* mixture_set, gmm_scorer_type type,
+                      const gmm_scorer_config* config, int device, gmm_scorer** out);
+int gmm_scorer_destroy(gmm_scorer* scorer);
+
+/* FeatureScorer::nMixtures() (FeatureScorer.hh:49), AssigningFeatureScorer::dimension(). */
+uint32_t gmm_scorer_n_mixtures(const gmm_scorer* scorer);
+uint32_t gmm_scorer_dimension(const gmm_scorer* scorer);
+int      gmm_scorer_type_of(const gmm_scorer* scorer);
+
+/* Score n_frames feature vectors (row t at frames + t * frame_stride floats)
+ * against every mixture of the handle's shard.  DEVICE pointers, enqueued on
+ * `stream` (a hipStream_t; NULL = default stream), asynchronous.
+ *   scores       [n_mixtures][score_stride] f32: ContextScorer::score(e) per frame
+ *   best_density [n_mixtures][score_stride] u32 or NULL: AssigningContextScorer::bestDensity(e)
+ *                (batch types have no assignment and ignore it).
+ * Replaces per-frame Context construction + calculateScoreAndDensity
+ * (SimdFeatureScorer.cc:22-35,135-176) and BatchFeatureScorerBase::fillScoreCache
+ * (BatchFeatureScorer.cc:98-105). */
+int gmm_score_device(gmm_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
+                     float* scores, uint32_t* best_density, uint32_t score_stride, void* stream);
+
+/* Same with HOST buffers (copies in, scores, copies out, synchronizes). */
+int gmm_score_host(gmm_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
+                   float* scores, uint32_t* best_density, uint32_t score_stride);
+
+/* SimdGaussDiagonalMaximumFeatureScorer accessors used by AcousticLookAhead
+ * (src/Search/AdvancedTreeSearch/AcousticLookAhead.cc:156,447):
+ * inverseQuantizationFactor() (SimdFeatureScorer.hh:128-130) and the
+ * quantization scale s (SimdFeatureScorer.cc:69).  Quantized types only. */
+int gmm_scorer_quantization(const gmm_scorer* scorer, float* scaling, float* inverse_quantization_factor);
+
+/* multiplyAndQuantize(featureVector) (SimdFeatureScorer.cc:37-52): out receives
+ * n_covariances x padded_dimension u8, padded_dimension = dimension rounded up to 16. */
+int gmm_scorer_multiply_and_quantize(const gmm_scorer* scorer, const float* feature, uint8_t* out);
+
+/* Host-side model preparation only (no device needed): the prepared tables
+ * of the SIMD / batch-int scorers, for CPU-side verification.
+ *   isv [n_covariances * dimension] scaled 1/sqrt(var); log_norm [n_covariances];
+ *   prepared_mean [n_entries * padded_dimension] u8; constant_weight [n_entries].
+ * Any output pointer may be NULL. */
+int gmm_prepare_quantized_host(const gmm_mixture_set* mixture_set, gmm_scorer_type type, float* scaling,
+                               float* isv, float* log_norm, uint8_t* prepared_mean, int32_t* constant_weight);
+
+/* Number of kernel launches one gmm_score_device call enqueues, and the name
+ * of the dominant kernel (for profiling scripts). */
+int gmm_scorer_launch_info(const gmm_scorer* scorer, uint32_t n_frames, uint32_t* n_launches,
+                           const char** main_kernel_name);
+
+/* Instrumentation for bench.py: when enabled, every gmm_score_* call records a
+ * pair of HIP events on its stream around the scorer kernel (the dominant
+ * launch); gmm_scorer_kernel_time synchronizes on the last event and returns
+ * the summed kernel time and launch count since the last reset. */
+int gmm_scorer_set_timing(gmm_scorer* scorer, int enable);
+int gmm_scorer_kernel_time(gmm_scorer* scorer, double* total_ms, uint32_t* n_launches, int reset);
+
+const char* gmm_last_error(void);
+const char* gmm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RASR_GMM_H */

@@ -1,0 +1,252 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes binding of oracle/_build/libgmm_oracle.so.
+
+CPU restatement of RASR's feature scorers (parity checker + CPU baseline).
+Parity status: UNPINNED (gmm_oracle.h explains why).  Works on any object with
+the MixtureSet attributes (means, variances, density_mean, density_covariance,
+mixture_offsets, mixture_densities, mixture_log_weights).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "_build", "libgmm_oracle.so")
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+
+
+class OrcMixtureSet(ctypes.Structure):
+    _fields_ = [("dimension", ctypes.c_uint32), ("n_means", ctypes.c_uint32), ("means", _f32p),
+                ("n_covariances", ctypes.c_uint32), ("variances", _f32p), ("n_densities", ctypes.c_uint32),
+                ("density_mean", _u32p), ("density_covariance", _u32p), ("n_mixtures", ctypes.c_uint32),
+                ("mixture_offsets", _u32p), ("mixture_densities", _u32p), ("mixture_log_weights", _f64p)]
+
+
+class OrcSimdModel(ctypes.Structure):
+    _fields_ = [("dimension", ctypes.c_uint32), ("padded_dimension", ctypes.c_uint32),
+                ("n_covariances", ctypes.c_uint32), ("n_entries", ctypes.c_uint32), ("scaling", ctypes.c_float),
+                ("scaling_squared", ctypes.c_float), ("inverse_quantization_factor", ctypes.c_float),
+                ("isv", _f32p), ("log_norm", _f32p), ("prepared_mean", ctypes.POINTER(ctypes.c_uint8)),
+                ("constant_weight", ctypes.POINTER(ctypes.c_int32)), ("entry_covariance", _u32p)]
+
+
+class OrcFloatModel(ctypes.Structure):
+    _fields_ = [("dimension", ctypes.c_uint32), ("n_covariances", ctypes.c_uint32), ("n_entries", ctypes.c_uint32),
+                ("isv", _f32p), ("log_norm", _f32p), ("minus2_log_weight", _f32p)]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    sig = {
+        "orc_inverse_sqrt": (ctypes.c_float, [ctypes.c_float]),
+        "orc_quantize": (ctypes.c_uint8, [ctypes.c_float]),
+        "orc_gauss_log_norm": (ctypes.c_double, [_f32p, ctypes.c_uint32]),
+        "orc_quantization_scaling_factor": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
+        "orc_constant_weight": (ctypes.c_int32, [ctypes.c_float, ctypes.c_double, ctypes.c_float]),
+        "orc_simd_final_score": (ctypes.c_float, [ctypes.c_int32, ctypes.c_float]),
+        "orc_batch_int_constant": (ctypes.c_int32, [ctypes.c_float, ctypes.c_float, ctypes.c_double]),
+        "orc_batch_int_final_score": (ctypes.c_float, [ctypes.c_int32, ctypes.c_float]),
+        "orc_float_distance": (ctypes.c_float, [_f32p, _f32p, _f32p, ctypes.c_uint32]),
+        "orc_simd_prepare": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), ctypes.POINTER(OrcSimdModel)]),
+        "orc_simd_free": (None, [ctypes.POINTER(OrcSimdModel)]),
+        "orc_simd_quantize_frame": (None, [ctypes.POINTER(OrcSimdModel), _f32p, _vp]),
+        "orc_simd_score": (ctypes.c_int, [ctypes.POINTER(OrcSimdModel), ctypes.POINTER(OrcMixtureSet), _vp,
+                                          ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int]),
+        "orc_float_prepare": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), ctypes.c_float, ctypes.c_float,
+                                             ctypes.POINTER(OrcFloatModel)]),
+        "orc_float_free": (None, [ctypes.POINTER(OrcFloatModel)]),
+        "orc_float_score": (ctypes.c_int, [ctypes.POINTER(OrcFloatModel), ctypes.POINTER(OrcMixtureSet), _vp,
+                                           ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_int]),
+        "orc_batch_int_score": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, ctypes.c_uint32,
+                                               ctypes.c_uint32, _vp, ctypes.c_int]),
+        "orc_batch_float_score": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, ctypes.c_uint32,
+                                                 ctypes.c_uint32, _vp, ctypes.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+class _Desc:
+    """Keeps contiguous copies alive and exposes the C descriptor."""
+
+    def __init__(self, ms):
+        self.means = np.ascontiguousarray(ms.means, dtype=np.float32)
+        self.variances = np.ascontiguousarray(ms.variances, dtype=np.float32)
+        self.dm = np.ascontiguousarray(ms.density_mean, dtype=np.uint32)
+        self.dc = np.ascontiguousarray(ms.density_covariance, dtype=np.uint32)
+        self.mo = np.ascontiguousarray(ms.mixture_offsets, dtype=np.uint32)
+        self.md = np.ascontiguousarray(ms.mixture_densities, dtype=np.uint32)
+        self.lw = np.ascontiguousarray(ms.mixture_log_weights, dtype=np.float64)
+        d = OrcMixtureSet()
+        d.dimension = self.means.shape[1]
+        d.n_means = self.means.shape[0]
+        d.means = self.means.ctypes.data_as(_f32p)
+        d.n_covariances = self.variances.shape[0]
+        d.variances = self.variances.ctypes.data_as(_f32p)
+        d.n_densities = self.dm.shape[0]
+        d.density_mean = self.dm.ctypes.data_as(_u32p)
+        d.density_covariance = self.dc.ctypes.data_as(_u32p)
+        d.n_mixtures = self.mo.shape[0] - 1
+        d.mixture_offsets = self.mo.ctypes.data_as(_u32p)
+        d.mixture_densities = self.md.ctypes.data_as(_u32p)
+        d.mixture_log_weights = self.lw.ctypes.data_as(_f64p)
+        self.c = d
+        self.n_mixtures = int(d.n_mixtures)
+        self.n_entries = int(self.mo[-1])
+
+
+def _frames(frames):
+    f = np.ascontiguousarray(frames, dtype=np.float32)
+    return f, f.shape[0], f.shape[1]
+
+
+class OracleSimd:
+    """SIMD-diagonal-maximum restated (SimdFeatureScorer.cc)."""
+
+    def __init__(self, ms):
+        self.lib = load()
+        self.d = _Desc(ms)
+        self.m = OrcSimdModel()
+        rc = self.lib.orc_simd_prepare(ctypes.byref(self.d.c), ctypes.byref(self.m))
+        if rc != 0:
+            raise ValueError("orc_simd_prepare failed")
+        D, Dp, C, E = self.m.dimension, self.m.padded_dimension, self.m.n_covariances, self.m.n_entries
+        self.scaling = self.m.scaling
+        self.scaling_squared = self.m.scaling_squared
+        self.inverse_quantization_factor = self.m.inverse_quantization_factor
+        self.isv = np.ctypeslib.as_array(self.m.isv, shape=(C * D,)).reshape(C, D).copy()
+        self.log_norm = np.ctypeslib.as_array(self.m.log_norm, shape=(C,)).copy()
+        self.prepared_mean = (np.ctypeslib.as_array(self.m.prepared_mean, shape=(E * Dp,)).reshape(E, Dp).copy()
+                              if E else np.zeros((0, Dp), np.uint8))
+        self.constant_weight = (np.ctypeslib.as_array(self.m.constant_weight, shape=(E,)).copy()
+                                if E else np.zeros(0, np.int32))
+
+    def __del__(self):
+        try:
+            self.lib.orc_simd_free(ctypes.byref(self.m))
+        except Exception:
+            pass
+
+    def quantize_frame(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        out = np.empty((self.m.n_covariances, self.m.padded_dimension), dtype=np.uint8)
+        self.lib.orc_simd_quantize_frame(ctypes.byref(self.m), x.ctypes.data_as(_f32p),
+                                         out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+    def score(self, frames, n_threads: int = 1):
+        f, n, stride = _frames(frames)
+        M = self.d.n_mixtures
+        scores = np.empty((M, n), np.float32)
+        best = np.empty((M, n), np.uint32)
+        raw = np.empty((M, n), np.int32)
+        self.lib.orc_simd_score(ctypes.byref(self.m), ctypes.byref(self.d.c), f.ctypes.data_as(_vp), n, stride,
+                                scores.ctypes.data_as(_vp), best.ctypes.data_as(_vp), raw.ctypes.data_as(_vp),
+                                int(n_threads))
+        return scores, best, raw
+
+
+class OracleFloat:
+    """diagonal-maximum restated (GaussDiagonalMaximumFeatureScorer.cc)."""
+
+    def __init__(self, ms, mixture_weight_scale: float = 1.0, gaussian_scale: float = 1.0):
+        self.lib = load()
+        self.d = _Desc(ms)
+        self.m = OrcFloatModel()
+        rc = self.lib.orc_float_prepare(ctypes.byref(self.d.c), mixture_weight_scale, gaussian_scale,
+                                        ctypes.byref(self.m))
+        if rc != 0:
+            raise ValueError("orc_float_prepare failed")
+
+    def __del__(self):
+        try:
+            self.lib.orc_float_free(ctypes.byref(self.m))
+        except Exception:
+            pass
+
+    def score(self, frames, n_threads: int = 1):
+        f, n, stride = _frames(frames)
+        M = self.d.n_mixtures
+        scores = np.empty((M, n), np.float32)
+        best = np.empty((M, n), np.uint32)
+        self.lib.orc_float_score(ctypes.byref(self.m), ctypes.byref(self.d.c), f.ctypes.data_as(_vp), n, stride,
+                                 scores.ctypes.data_as(_vp), best.ctypes.data_as(_vp), int(n_threads))
+        return scores, best
+
+
+def batch_int_score(ms, frames, n_threads: int = 1):
+    lib = load()
+    d = _Desc(ms)
+    f, n, stride = _frames(frames)
+    scores = np.empty((d.n_mixtures, n), np.float32)
+    if lib.orc_batch_int_score(ctypes.byref(d.c), f.ctypes.data_as(_vp), n, stride, scores.ctypes.data_as(_vp),
+                               int(n_threads)) != 0:
+        raise ValueError("orc_batch_int_score failed")
+    return scores
+
+
+def batch_float_score(ms, frames, n_threads: int = 1):
+    lib = load()
+    d = _Desc(ms)
+    f, n, stride = _frames(frames)
+    scores = np.empty((d.n_mixtures, n), np.float32)
+    if lib.orc_batch_float_score(ctypes.byref(d.c), f.ctypes.data_as(_vp), n, stride, scores.ctypes.data_as(_vp),
+                                 int(n_threads)) != 0:
+        raise ValueError("orc_batch_float_score failed")
+    return scores
+
+
+def inverse_sqrt(x: float) -> float:
+    return load().orc_inverse_sqrt(x)
+
+
+def quantize(x: float) -> int:
+    return load().orc_quantize(x)
+
+
+def gauss_log_norm(v) -> float:
+    v = np.ascontiguousarray(v, dtype=np.float32)
+    return load().orc_gauss_log_norm(v.ctypes.data_as(_f32p), v.shape[0])
+
+
+def quantization_scaling_factor(a: float, b: float) -> float:
+    return load().orc_quantization_scaling_factor(a, b)
+
+
+def constant_weight(s2: float, logw: float, lognorm: float) -> int:
+    return load().orc_constant_weight(s2, logw, lognorm)
+
+
+def simd_final_score(q: int, s2: float) -> float:
+    return load().orc_simd_final_score(q, s2)
+
+
+def float_distance(feature, mean, isv) -> float:
+    f = np.ascontiguousarray(feature, np.float32)
+    m = np.ascontiguousarray(mean, np.float32)
+    i = np.ascontiguousarray(isv, np.float32)
+    return load().orc_float_distance(f.ctypes.data_as(_f32p), m.ctypes.data_as(_f32p), i.ctypes.data_as(_f32p),
+                                     f.shape[0])

@@ -1,0 +1,126 @@
+"""ctypes binding of the C-ABI in include/rasr_gmm.h (librasr_gmm.so).
+
+The library is the product: there is no Python or CPU fallback.  If the shared
+object is missing, loading raises immediately (build it with `make` or
+`python -c "import __graft_entry__ as g; g.build()"`).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "librasr_gmm.so")
+
+GMM_OK = 0
+
+# Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
+BATCH_DIAGONAL_MAXIMUM_FLOAT = 0
+BATCH_DIAGONAL_MAXIMUM_INT = 3
+BATCH_DIAGONAL_MAXIMUM_FAST = 4
+DIAGONAL_MAXIMUM = 5
+SIMD_DIAGONAL_MAXIMUM = 9
+
+SCORER_TYPES = {
+    "batch-diagonal-maximum-float": BATCH_DIAGONAL_MAXIMUM_FLOAT,
+    "batch-diagonal-maximum-int": BATCH_DIAGONAL_MAXIMUM_INT,
+    "batch-diagonal-maximum-fast": BATCH_DIAGONAL_MAXIMUM_FAST,
+    "diagonal-maximum": DIAGONAL_MAXIMUM,
+    "SIMD-diagonal-maximum": SIMD_DIAGONAL_MAXIMUM,
+}
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+class MixtureSetDesc(ctypes.Structure):
+    _fields_ = [
+        ("dimension", ctypes.c_uint32),
+        ("n_means", ctypes.c_uint32),
+        ("means", _f32p),
+        ("n_covariances", ctypes.c_uint32),
+        ("variances", _f32p),
+        ("n_densities", ctypes.c_uint32),
+        ("density_mean", _u32p),
+        ("density_covariance", _u32p),
+        ("n_mixtures", ctypes.c_uint32),
+        ("mixture_offsets", _u32p),
+        ("mixture_densities", _u32p),
+        ("mixture_log_weights", _f64p),
+    ]
+
+
+class ScorerConfig(ctypes.Structure):
+    _fields_ = [
+        ("mixture_weight_scale", ctypes.c_float),
+        ("gaussian_scale", ctypes.c_float),
+        ("score_scale", ctypes.c_float),
+        ("max_frames", ctypes.c_uint32),
+        ("mixture_begin", ctypes.c_uint32),
+        ("mixture_end", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
+# (name, restype, argtypes) for every function declared in include/rasr_gmm.h
+PROTOTYPES = [
+    ("gmm_default_config", None, [ctypes.POINTER(ScorerConfig)]),
+    ("gmm_scorer_create", ctypes.c_int,
+     [ctypes.POINTER(MixtureSetDesc), ctypes.c_int, ctypes.POINTER(ScorerConfig), ctypes.c_int,
+      ctypes.POINTER(ctypes.c_void_p)]),
+    ("gmm_scorer_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("gmm_scorer_n_mixtures", ctypes.c_uint32, [ctypes.c_void_p]),
+    ("gmm_scorer_dimension", ctypes.c_uint32, [ctypes.c_void_p]),
+    ("gmm_scorer_type_of", ctypes.c_int, [ctypes.c_void_p]),
+    ("gmm_score_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_uint32, ctypes.c_void_p]),
+    ("gmm_score_host", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_uint32]),
+    ("gmm_scorer_quantization", ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p]),
+    ("gmm_scorer_multiply_and_quantize", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("gmm_prepare_quantized_host", ctypes.c_int,
+     [ctypes.POINTER(MixtureSetDesc), ctypes.c_int, _f32p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p]),
+    ("gmm_scorer_launch_info", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, _u32p, ctypes.POINTER(ctypes.c_char_p)]),
+    ("gmm_scorer_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("gmm_scorer_kernel_time", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), _u32p, ctypes.c_int]),
+    ("gmm_last_error", ctypes.c_char_p, []),
+    ("gmm_version", ctypes.c_char_p, []),
+]
+
+_lib = None
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load librasr_gmm.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"rasr_amd native library not found at {p}: the MI355X scorer has no fallback; "
+            "build it with `make` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(p)
+    for name, res, args in PROTOTYPES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class GmmError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != GMM_OK:
+        msg = load_library().gmm_last_error()
+        raise GmmError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,537 @@
+// gmm_api.cc -- C-ABI of the MI355X GMM feature scorer (include/rasr_gmm.h).
+//
+// One handle = one prepared model resident on one GPU (tiles, row constants,
+// scaled inverse deviations) plus frame staging buffers sized for
+// config.max_frames.  gmm_score_device enqueues two kernels on the caller's
+// stream: the frame preparation (quantize / scale the feature vectors, the
+// per-frame Context of the reference, SimdFeatureScorer.cc:22-35) and the
+// scorer.  No host synchronisation, no allocation on that path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rasr_gmm.h"
+#include "gmm_kernels.hh"
+#include "gmm_prepare.hh"
+
+using namespace rasr_gmm;
+
+namespace {
+
+thread_local std::string gLastError;
+
+int fail(int code, const std::string& msg) {
+    gLastError = msg;
+    return code;
+}
+
+#define GMM_HIP_CHECK(expr)                                                                         \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess)                                                                       \
+            return fail(GMM_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+template <class T>
+int upload(T** dst, const std::vector<T>& src, size_t padElems = 0) {
+    const size_t n = src.size() + padElems;
+    if (n == 0) {
+        *dst = nullptr;
+        return GMM_OK;
+    }
+    GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dst), n * sizeof(T)));
+    GMM_HIP_CHECK(hipMemset(*dst, 0, n * sizeof(T)));
+    if (!src.empty())
+        GMM_HIP_CHECK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return GMM_OK;
+}
+
+struct ChunkTable {
+    uint32_t  nChunks = 0;
+    uint32_t* dMixOff = nullptr;
+};
+
+}  // namespace
+
+struct gmm_scorer {
+    gmm_scorer_type   type;
+    Flavor            flavor;
+    bool              quantized = false;
+    int               device    = 0;
+    gmm_scorer_config cfg{};
+    uint32_t          D = 0, C = 0, nMix = 0, mixBase = 0, nTiles = 0, kSteps = 0;
+    uint32_t          nFramesPad = 0;
+    bool              multiCov   = false;
+    bool              foldNorm   = false;
+    // quantized scalars
+    uint32_t idxBits = 1, paddedDimension = 0;
+    float    scaling = 0, scalingSquared = 0, invQ = 0, batchScale = 0;
+    std::vector<float>    isvScaled;     // [C][D] (quantized types)
+    std::vector<uint32_t> mixTileOff;    // host copy
+    // device model
+    void*     dTileA     = nullptr;
+    void*     dTileP     = nullptr;
+    uint32_t* dTileCov   = nullptr;
+    uint32_t* dRowDns    = nullptr;
+    uint32_t* dMixTileOff = nullptr;
+    float*    dIsv       = nullptr;
+    // device frame staging
+    int8_t*  dFrameQ  = nullptr;
+    int32_t* dFrameSS = nullptr;
+    float*   dFrameX  = nullptr;
+    float*   dFrameXX = nullptr;
+    // host-API staging
+    float*    dHostFrames = nullptr;
+    float*    dHostScores = nullptr;
+    uint32_t* dHostBest   = nullptr;
+    std::map<uint32_t, ChunkTable> chunks;  // keyed by frame tiles per call
+    // kernel timing (gmm_scorer_set_timing)
+    bool                                        timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    size_t                                      eventsUsed = 0;
+
+    ~gmm_scorer() {
+        void* ptrs[] = {dTileA,  dTileP,  dTileCov, dRowDns,     dMixTileOff, dIsv,     dFrameQ,
+                        dFrameSS, dFrameX, dFrameXX, dHostFrames, dHostScores, dHostBest};
+        for (void* p : ptrs)
+            if (p)
+                (void)hipFree(p);
+        for (auto& kv : chunks)
+            if (kv.second.dMixOff)
+                (void)hipFree(kv.second.dMixOff);
+        for (auto& ev : events) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+    }
+};
+
+namespace {
+
+uint32_t framesPerBlock(const gmm_scorer* s) {
+    return s->quantized ? kI8FramesPerBlock : kF32FramesPerBlock;
+}
+
+// Cut the shard's mixtures into chunks of about equal tile count so that
+// chunks x frame-tiles gives enough workgroups to fill 256 CUs several times.
+int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
+    auto it = s->chunks.find(nFrameTiles);
+    if (it != s->chunks.end()) {
+        *out = &it->second;
+        return GMM_OK;
+    }
+    const uint32_t kTargetBlocks = 8192;
+    uint32_t       target        = std::max<uint32_t>(1, (kTargetBlocks + nFrameTiles - 1) / nFrameTiles);
+    target                       = std::min<uint32_t>(target, std::max<uint32_t>(1, s->nMix));
+    const uint32_t T             = s->nTiles;
+    const uint32_t perChunk      = std::max<uint32_t>(1, (T + target - 1) / target);
+    std::vector<uint32_t> off{0};
+    uint32_t              acc = 0;
+    for (uint32_t m = 0; m < s->nMix; ++m) {
+        acc += s->mixTileOff[m + 1] - s->mixTileOff[m];
+        if (acc >= perChunk && m + 1 < s->nMix) {
+            off.push_back(m + 1);
+            acc = 0;
+        }
+    }
+    off.push_back(s->nMix);
+    ChunkTable ct;
+    ct.nChunks = static_cast<uint32_t>(off.size() - 1);
+    int rc     = upload(&ct.dMixOff, off);
+    if (rc != GMM_OK)
+        return rc;
+    auto ins = s->chunks.emplace(nFrameTiles, ct);
+    *out     = &ins.first->second;
+    return GMM_OK;
+}
+
+// HIP events around the scorer kernel, on the kernel's own stream (bench.py roofline timing).
+struct TimedSpan {
+    gmm_scorer* s;
+    hipStream_t stream;
+    hipEvent_t  b = nullptr, e = nullptr;
+    TimedSpan(gmm_scorer* sc, hipStream_t st) : s(sc), stream(st) {}
+    hipError_t begin() {
+        if (!s->timing)
+            return hipSuccess;
+        if (s->eventsUsed == s->events.size()) {
+            hipEvent_t x, y;
+            hipError_t err = hipEventCreate(&x);
+            if (err != hipSuccess)
+                return err;
+            if ((err = hipEventCreate(&y)) != hipSuccess)
+                return err;
+            s->events.emplace_back(x, y);
+        }
+        b = s->events[s->eventsUsed].first;
+        e = s->events[s->eventsUsed].second;
+        ++s->eventsUsed;
+        return hipEventRecord(b, stream);
+    }
+    hipError_t end() { return s->timing ? hipEventRecord(e, stream) : hipSuccess; }
+};
+
+int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+              uint32_t* best, uint32_t scoreStride, hipStream_t stream) {
+    if (nFrames == 0 || s->nMix == 0)
+        return GMM_OK;
+    if (nFrames > s->cfg.max_frames)
+        return fail(GMM_ERR_CAPACITY, "n_frames exceeds config.max_frames");
+    if (!frames || !scores || frameStride < s->D || scoreStride < nFrames)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frames/scores/stride");
+    GMM_HIP_CHECK(hipSetDevice(s->device));
+    const uint32_t fpb         = framesPerBlock(s);
+    const uint32_t nFrameTiles = (nFrames + fpb - 1) / fpb;
+    const uint32_t nPadCall    = nFrameTiles * fpb;  // rows the scorer reads
+    const ChunkTable* ct       = nullptr;
+    int               rc       = chunkTableFor(s, nFrameTiles, &ct);
+    if (rc != GMM_OK)
+        return rc;
+    if (s->quantized) {
+        GMM_HIP_CHECK(launchPrepareFramesI8(frames, nFrames, frameStride, s->nFramesPad, nPadCall, s->D, s->C,
+                                            s->kSteps, s->dIsv, s->dFrameQ, s->dFrameSS, stream));
+        I8Args a{};
+        a.tileA       = s->dTileA;
+        a.tileP       = s->dTileP;
+        a.tileCov     = s->dTileCov;
+        a.mixTileOff  = s->dMixTileOff;
+        a.chunkMixOff = ct->dMixOff;
+        a.frameQ      = s->dFrameQ;
+        a.frameSS     = s->dFrameSS;
+        a.scores      = scores;
+        a.best        = s->flavor == Flavor::Simd ? best : nullptr;
+        a.nFrames     = nFrames;
+        a.nFramesPad  = s->nFramesPad;
+        a.scoreStride = scoreStride;
+        a.nChunks     = ct->nChunks;
+        a.nFrameTiles = nFrameTiles;
+        a.mixBase     = 0;
+        a.idxBits     = s->idxBits;
+        a.flavor      = s->flavor == Flavor::Simd ? 0 : 1;
+        a.s2          = s->scalingSquared;
+        a.batchScale  = s->batchScale;
+        a.outScale    = s->cfg.score_scale;
+        TimedSpan span(s, stream);
+        GMM_HIP_CHECK(span.begin());
+        GMM_HIP_CHECK(launchScoreI8(a, s->kSteps, s->multiCov, stream));
+        GMM_HIP_CHECK(span.end());
+    }
+    else {
+        GMM_HIP_CHECK(launchPrepareFramesF32(frames, nFrames, frameStride, s->nFramesPad, nPadCall, s->D, s->C, s->kSteps,
+                                             s->foldNorm ? 1 : 0, s->dIsv, s->dFrameX, s->dFrameXX, stream));
+        F32Args a{};
+        a.tileA       = static_cast<const float*>(s->dTileA);
+        a.tileCov     = s->dTileCov;
+        a.rowDns      = s->dRowDns;
+        a.mixTileOff  = s->dMixTileOff;
+        a.chunkMixOff = ct->dMixOff;
+        a.frameX      = s->dFrameX;
+        a.frameXX     = s->dFrameXX;
+        a.scores      = scores;
+        a.best        = s->flavor == Flavor::DiagonalMaximum ? best : nullptr;
+        a.nFrames     = nFrames;
+        a.nFramesPad  = s->nFramesPad;
+        a.scoreStride = scoreStride;
+        a.nChunks     = ct->nChunks;
+        a.nFrameTiles = nFrameTiles;
+        a.mixBase     = 0;
+        a.flavor      = s->flavor == Flavor::DiagonalMaximum ? 2 : 3;
+        a.outScale    = s->cfg.score_scale;
+        TimedSpan span(s, stream);
+        GMM_HIP_CHECK(span.begin());
+        GMM_HIP_CHECK(launchScoreF32(a, s->kSteps, s->multiCov, stream));
+        GMM_HIP_CHECK(span.end());
+    }
+    return GMM_OK;
+}
+
+Flavor flavorOf(gmm_scorer_type t, bool* quantized, bool* ok) {
+    *ok = true;
+    switch (t) {
+        case GMM_SIMD_DIAGONAL_MAXIMUM: *quantized = true; return Flavor::Simd;
+        case GMM_BATCH_DIAGONAL_MAXIMUM_INT:
+        case GMM_BATCH_DIAGONAL_MAXIMUM_FAST: *quantized = true; return Flavor::BatchInt;
+        case GMM_DIAGONAL_MAXIMUM: *quantized = false; return Flavor::DiagonalMaximum;
+        case GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT: *quantized = false; return Flavor::BatchFloat;
+    }
+    *ok = false;
+    return Flavor::Simd;
+}
+
+}  // namespace
+
+extern "C" {
+
+void gmm_default_config(gmm_scorer_config* cfg) {
+    if (!cfg)
+        return;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->mixture_weight_scale = 1.0f;
+    cfg->gaussian_scale       = 1.0f;
+    cfg->score_scale          = 1.0f;
+    cfg->max_frames           = 4;  // "buffer-size" default, BatchFeatureScorer.cc:28-29
+}
+
+int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scorer_config* config,
+                      int device, gmm_scorer** out) {
+    if (!ms || !out)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    bool   quantized = false, ok = false;
+    Flavor flavor    = flavorOf(type, &quantized, &ok);
+    if (!ok)
+        return fail(GMM_ERR_UNSUPPORTED, "unknown feature scorer type");
+    gmm_scorer_config cfg;
+    gmm_default_config(&cfg);
+    if (config)
+        cfg = *config;
+    if (cfg.max_frames == 0)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "max_frames must be > 0");
+    if (type == GMM_BATCH_DIAGONAL_MAXIMUM_FAST && (ms->dimension + 15) / 16 * 16 > 48)
+        return fail(GMM_ERR_UNSUPPORTED, "This feature scorer supports only features with max. 48 components");
+    ShardRange shard{cfg.mixture_begin, cfg.mixture_end};
+
+    auto s      = std::make_unique<gmm_scorer>();
+    s->type     = type;
+    s->flavor   = flavor;
+    s->quantized = quantized;
+    s->device   = device;
+    s->cfg      = cfg;
+    s->D        = ms->dimension;
+    s->C        = ms->n_covariances;
+    s->nFramesPad = (cfg.max_frames + kFramePadQuantum - 1) / kFramePadQuantum * kFramePadQuantum;
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(GMM_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "device index out of range");
+    GMM_HIP_CHECK(hipSetDevice(device));
+
+    const Tiling* tiling = nullptr;
+    int           rc     = GMM_OK;
+    if (quantized) {
+        PreparedQuantized p;
+        std::string       err = prepareQuantized(*ms, flavor, shard, p);
+        if (!err.empty())
+            return fail(GMM_ERR_INVALID_ARGUMENT, err);
+        s->nMix            = p.nMixtures;
+        s->kSteps          = p.kSteps;
+        s->idxBits         = p.idxBits;
+        s->paddedDimension = p.paddedDimension;
+        s->scaling         = p.scaling;
+        s->scalingSquared  = p.scalingSquared;
+        s->invQ            = p.inverseQuantizationFactor;
+        s->batchScale      = p.batchScale;
+        s->isvScaled       = p.isvScaled;
+        s->multiCov        = s->C > 1;
+        s->nTiles          = p.tiling.nTiles;
+        s->mixTileOff      = p.tiling.mixTileOffset;
+        // one zero padding tile so the kernels may prefetch tile t+1 unconditionally
+        if ((rc = upload(reinterpret_cast<int8_t**>(&s->dTileA), p.tileA, kLanes * 16 * p.kSteps)) ||
+            (rc = upload(reinterpret_cast<int32_t**>(&s->dTileP), p.tileP, kTileRows)) ||
+            (rc = upload(&s->dTileCov, p.tiling.tileCovariance, 1)) || (rc = upload(&s->dMixTileOff, s->mixTileOff)) ||
+            (rc = upload(&s->dIsv, p.isvDevice)))
+            return rc;
+        const size_t nQ = static_cast<size_t>(s->C) * s->nFramesPad;
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameQ), nQ * s->kSteps * kI8K));
+        GMM_HIP_CHECK(hipMemset(s->dFrameQ, 0, nQ * s->kSteps * kI8K));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameSS), nQ * sizeof(int32_t)));
+        GMM_HIP_CHECK(hipMemset(s->dFrameSS, 0, nQ * sizeof(int32_t)));
+        (void)tiling;
+    }
+    else {
+        PreparedFloat p;
+        std::string   err = prepareFloat(*ms, flavor, cfg.mixture_weight_scale, cfg.gaussian_scale, shard, p);
+        if (!err.empty())
+            return fail(GMM_ERR_INVALID_ARGUMENT, err);
+        s->nMix       = p.nMixtures;
+        s->kSteps     = p.kSteps;
+        s->multiCov   = s->C > 1;
+        s->foldNorm   = p.foldNorm;
+        s->nTiles     = p.tiling.nTiles;
+        s->mixTileOff = p.tiling.mixTileOffset;
+        if ((rc = upload(reinterpret_cast<float**>(&s->dTileA), p.tileA, kLanes * p.kSteps)) ||
+            (rc = upload(&s->dTileCov, p.tiling.tileCovariance, 1)) ||
+            (rc = upload(&s->dRowDns, p.tiling.rowDensityInMixture, kTileRows)) ||
+            (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)))
+            return rc;
+        const size_t nX = static_cast<size_t>(s->C) * s->nFramesPad;
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameX), nX * s->kSteps * 4 * sizeof(float)));
+        GMM_HIP_CHECK(hipMemset(s->dFrameX, 0, nX * s->kSteps * 4 * sizeof(float)));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameXX), nX * sizeof(float)));
+        GMM_HIP_CHECK(hipMemset(s->dFrameXX, 0, nX * sizeof(float)));
+    }
+    s->mixBase = shard.begin == 0 && shard.end == 0 ? 0 : shard.begin;
+    GMM_HIP_CHECK(hipDeviceSynchronize());
+    *out = s.release();
+    return GMM_OK;
+}
+
+int gmm_scorer_destroy(gmm_scorer* s) {
+    if (!s)
+        return GMM_OK;
+    (void)hipSetDevice(s->device);
+    delete s;
+    return GMM_OK;
+}
+
+uint32_t gmm_scorer_n_mixtures(const gmm_scorer* s) {
+    return s ? s->nMix : 0;
+}
+
+uint32_t gmm_scorer_dimension(const gmm_scorer* s) {
+    return s ? s->D : 0;
+}
+
+int gmm_scorer_type_of(const gmm_scorer* s) {
+    return s ? static_cast<int>(s->type) : -1;
+}
+
+int gmm_score_device(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+                     uint32_t* best, uint32_t scoreStride, void* stream) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    return scoreImpl(s, frames, nFrames, frameStride, scores, best, scoreStride, static_cast<hipStream_t>(stream));
+}
+
+int gmm_score_host(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+                   uint32_t* best, uint32_t scoreStride) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    if (nFrames == 0)
+        return GMM_OK;
+    if (nFrames > s->cfg.max_frames)
+        return fail(GMM_ERR_CAPACITY, "n_frames exceeds config.max_frames");
+    if (!frames || !scores || frameStride < s->D || scoreStride < nFrames)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frames/scores/stride");
+    GMM_HIP_CHECK(hipSetDevice(s->device));
+    const size_t maxF = s->cfg.max_frames;
+    if (!s->dHostFrames) {
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostFrames), maxF * s->D * sizeof(float)));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostScores), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(float)));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostBest), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(uint32_t)));
+    }
+    GMM_HIP_CHECK(hipMemcpy2D(s->dHostFrames, s->D * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
+                              s->D * sizeof(float), nFrames, hipMemcpyHostToDevice));
+    int rc = scoreImpl(s, s->dHostFrames, nFrames, s->D, s->dHostScores, best ? s->dHostBest : nullptr, nFrames, nullptr);
+    if (rc != GMM_OK)
+        return rc;
+    GMM_HIP_CHECK(hipDeviceSynchronize());
+    GMM_HIP_CHECK(hipMemcpy2D(scores, static_cast<size_t>(scoreStride) * sizeof(float), s->dHostScores,
+                              static_cast<size_t>(nFrames) * sizeof(float), static_cast<size_t>(nFrames) * sizeof(float),
+                              s->nMix, hipMemcpyDeviceToHost));
+    if (best)
+        GMM_HIP_CHECK(hipMemcpy2D(best, static_cast<size_t>(scoreStride) * sizeof(uint32_t), s->dHostBest,
+                                  static_cast<size_t>(nFrames) * sizeof(uint32_t),
+                                  static_cast<size_t>(nFrames) * sizeof(uint32_t), s->nMix, hipMemcpyDeviceToHost));
+    return GMM_OK;
+}
+
+int gmm_scorer_quantization(const gmm_scorer* s, float* scaling, float* invQ) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    if (!s->quantized)
+        return fail(GMM_ERR_UNSUPPORTED, "scorer type is not quantized");
+    if (scaling)
+        *scaling = s->scaling;
+    if (invQ)
+        *invQ = s->invQ;
+    return GMM_OK;
+}
+
+int gmm_scorer_multiply_and_quantize(const gmm_scorer* s, const float* feature, uint8_t* out) {
+    if (!s || !feature || !out)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    if (!s->quantized)
+        return fail(GMM_ERR_UNSUPPORTED, "scorer type is not quantized");
+    const uint32_t Dp = s->paddedDimension;
+    for (uint32_t c = 0; c < s->C; ++c) {
+        uint8_t* r = out + static_cast<size_t>(c) * Dp;
+        for (uint32_t k = 0; k < s->D; ++k)
+            r[k] = refQuantize(feature[k] * s->isvScaled[static_cast<size_t>(c) * s->D + k]);
+        for (uint32_t k = s->D; k < Dp; ++k)
+            r[k] = 0;
+    }
+    return GMM_OK;
+}
+
+int gmm_prepare_quantized_host(const gmm_mixture_set* ms, gmm_scorer_type type, float* scaling, float* isv,
+                               float* logNorm, uint8_t* preparedMean, int32_t* constantWeight) {
+    if (!ms)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null mixture set");
+    bool   quantized = false, ok = false;
+    Flavor flavor    = flavorOf(type, &quantized, &ok);
+    if (!ok || !quantized)
+        return fail(GMM_ERR_UNSUPPORTED, "type is not a quantized scorer");
+    PreparedQuantized p;
+    std::string       err = prepareQuantized(*ms, flavor, ShardRange{}, p);
+    if (!err.empty())
+        return fail(GMM_ERR_INVALID_ARGUMENT, err);
+    if (scaling)
+        *scaling = p.scaling;
+    if (isv)
+        std::copy(p.isvScaled.begin(), p.isvScaled.end(), isv);
+    if (logNorm)
+        std::copy(p.logNormScaled.begin(), p.logNormScaled.end(), logNorm);
+    if (preparedMean)
+        std::copy(p.preparedMean.begin(), p.preparedMean.end(), preparedMean);
+    if (constantWeight)
+        std::copy(p.constantWeight.begin(), p.constantWeight.end(), constantWeight);
+    return GMM_OK;
+}
+
+int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLaunches, const char** name) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    (void)nFrames;
+    if (nLaunches)
+        *nLaunches = 2;
+    if (name)
+        *name = s->quantized ? "scoreI8" : "scoreF32";
+    return GMM_OK;
+}
+
+int gmm_scorer_set_timing(gmm_scorer* s, int enable) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    s->timing     = enable != 0;
+    s->eventsUsed = 0;
+    return GMM_OK;
+}
+
+int gmm_scorer_kernel_time(gmm_scorer* s, double* totalMs, uint32_t* nLaunches, int reset) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    GMM_HIP_CHECK(hipSetDevice(s->device));
+    double total = 0;
+    for (size_t i = 0; i < s->eventsUsed; ++i) {
+        GMM_HIP_CHECK(hipEventSynchronize(s->events[i].second));
+        float ms = 0;
+        GMM_HIP_CHECK(hipEventElapsedTime(&ms, s->events[i].first, s->events[i].second));
+        total += ms;
+    }
+    if (totalMs)
+        *totalMs = total;
+    if (nLaunches)
+        *nLaunches = static_cast<uint32_t>(s->eventsUsed);
+    if (reset)
+        s->eventsUsed = 0;
+    return GMM_OK;
+}
+
+const char* gmm_last_error(void) {
+    return gLastError.c_str();
+}
+
+const char* gmm_version(void) {
+    return "rasr_amd-gmm 0.1 (gfx950)";
+}
+
+}  // extern "C"

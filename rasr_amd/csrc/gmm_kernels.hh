@@ -1,0 +1,59 @@
+// gmm_kernels.hh -- launch interface of the MI355X GMM scorer kernels (gmm_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rasr_gmm {
+
+constexpr int      kI8NF          = 8;   // column blocks of 16 frames per wave, quantized kernel
+constexpr int      kF32NF         = 4;   // column blocks of 16 frames per wave, float kernel
+constexpr uint32_t kWavesPerBlock = 4;
+constexpr uint32_t kI8FramesPerBlock  = kWavesPerBlock * kI8NF * 16;   // 512
+constexpr uint32_t kF32FramesPerBlock = kWavesPerBlock * kF32NF * 16;  // 256
+constexpr uint32_t kFramePadQuantum   = 512;
+
+struct I8Args {
+    const void*     tileA;        // i32x4 [T+1][KS][64]
+    const void*     tileP;        // i32x4 [T+1][4]
+    const uint32_t* tileCov;      // [T+1]
+    const uint32_t* mixTileOff;   // [nMixtures+1]
+    const uint32_t* chunkMixOff;  // [nChunks+1]
+    const int8_t*   frameQ;       // [C][nFramesPad][KS*64]
+    const int32_t*  frameSS;      // [C][nFramesPad]
+    float*          scores;
+    uint32_t*       best;
+    uint32_t        nFrames, nFramesPad, scoreStride;
+    uint32_t        nChunks, nFrameTiles, mixBase;
+    uint32_t        idxBits;
+    int             flavor;       // 0 SIMD-diagonal-maximum, 1 batch-int
+    float           s2, batchScale, outScale;
+};
+
+struct F32Args {
+    const float*    tileA;        // [T+1][KS][64]
+    const uint32_t* tileCov;      // [T+1]
+    const uint32_t* rowDns;       // [T+1][16]
+    const uint32_t* mixTileOff;
+    const uint32_t* chunkMixOff;
+    const float*    frameX;       // [C][nFramesPad/16][KS][64]
+    const float*    frameXX;      // [C][nFramesPad]
+    float*          scores;
+    uint32_t*       best;
+    uint32_t        nFrames, nFramesPad, scoreStride;
+    uint32_t        nChunks, nFrameTiles, mixBase;
+    int             flavor;       // 2 diagonal-maximum, 3 batch-float
+    float           outScale;
+};
+
+hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
+                                 uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, const float* isv, int8_t* frameQ,
+                                 int32_t* frameSS, hipStream_t stream);
+hipError_t launchPrepareFramesF32(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
+                                  uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, int foldNorm, const float* isv, float* frameX,
+                                  float* frameXX, hipStream_t stream);
+hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
+hipError_t launchScoreF32(const F32Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
+
+}  // namespace rasr_gmm

@@ -1,0 +1,403 @@
+// gmm_prepare.cc -- host-side model preparation (see gmm_prepare.hh).
+//
+// Every scalar formula below restates the reference expression as the
+// reference binary computes it: built with -O2 -ffast-math -msse3
+// (config/cc-gcc.make, config/proc-x86_64.make), GCC turns some of them into
+// specific instruction sequences (rsqrtss + Newton-Raphson for 1/sqrt, an
+// add-0.49999997-and-truncate for round, a float division for the quantization
+// scale).  They are written out explicitly here so this file gives the same
+// bits whatever flags it is compiled with.
+#include "gmm_prepare.hh"
+
+#include <xmmintrin.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+
+namespace rasr_gmm {
+
+// ---------------------------------------------------------------------------
+// scalar arithmetic
+// ---------------------------------------------------------------------------
+
+// inverseSquareRoot<f32> (src/Mm/Utilities.hh:87-91) compiled with -ffast-math:
+//   y = rsqrtss(x); r = ((x*y)*y + -3) * (y * -0.5)
+// rsqrtss is the host CPU's own approximation, exactly as in the reference binary.
+float refInverseSqrt(float x) {
+    __m128 vx = _mm_set_ss(x);
+    __m128 y  = _mm_rsqrt_ss(vx);
+    __m128 t  = _mm_mul_ss(_mm_mul_ss(vx, y), y);
+    __m128 u  = _mm_mul_ss(y, _mm_set_ss(-0.5f));
+    t         = _mm_add_ss(t, _mm_set_ss(-3.0f));
+    return _mm_cvtss_f32(_mm_mul_ss(t, u));
+}
+
+// (s32)float with x86 cvttss2si semantics: truncation, 0x80000000 when out of range / NaN.
+int32_t refTruncF32(float x) {
+    if (!(std::fabs(x) < 2147483648.0f))
+        return std::numeric_limits<int32_t>::min();
+    return static_cast<int32_t>(x);
+}
+
+int32_t refTruncF64(double x) {
+    if (!(x > -2147483649.0 && x < 2147483648.0))
+        return std::numeric_limits<int32_t>::min();
+    return static_cast<int32_t>(x);
+}
+
+// (int)round(x), src/Mm/Utilities.hh:189, as built: t = x + copysign(nextbelow(0.5), x); cvttss2si(t).
+int32_t refRoundToInt(float x) {
+    const float h = std::copysign(0x1.fffffep-2f, x);  // 0.49999997f
+    return refTruncF32(x + h);
+}
+
+// quantize<f32,u8>::operator() (Utilities.hh:186-190): clip((int)round(x) + 128) to [0,255].
+// The +128 is a 32-bit wrapping add in the reference binary.
+uint8_t refQuantize(float x) {
+    int32_t v = static_cast<int32_t>(static_cast<uint32_t>(refRoundToInt(x)) + 128u);
+    if (v > 255)
+        v = 255;
+    if (v < 0)
+        v = 0;
+    return static_cast<uint8_t>(v);
+}
+
+// gaussLogNormFactor (Utilities.hh:55-76): D*log(2 pi) + sum log|v| in double, in order.
+// log(2 pi) is the constant GCC folds at compile time.
+double refGaussLogNorm(const float* var, uint32_t d) {
+    double result = 0;
+    for (uint32_t i = 0; i < d; ++i)
+        result += std::log(static_cast<double>(std::fabs(var[i])));
+    return static_cast<double>(d) * 0x1.d67f1c864beb4p+0 + result;
+}
+
+// quantizationScalingFactor (SimdFeatureScorer.cc:128-133), as built: 255/(1.25*2*m) folds to
+// the single-precision division 102.0f / m.
+float refQuantizationScalingFactor(float minv, float maxv) {
+    float a = std::fabs(minv), b = std::fabs(maxv);
+    float m = a < b ? b : a;
+    return 102.0f / m;
+}
+
+// ---------------------------------------------------------------------------
+// validation and tiling
+// ---------------------------------------------------------------------------
+
+std::string validate(const gmm_mixture_set& ms) {
+    if (ms.dimension == 0)
+        return "dimension must be > 0";
+    if (!ms.means || !ms.variances || !ms.density_mean || !ms.density_covariance || !ms.mixture_offsets ||
+        (!ms.mixture_densities && ms.n_mixtures && ms.mixture_offsets[ms.n_mixtures]) ||
+        (!ms.mixture_log_weights && ms.n_mixtures && ms.mixture_offsets[ms.n_mixtures]))
+        return "null table in mixture set";
+    if (ms.n_covariances == 0)
+        return "mixture set has no covariance";
+    if (ms.mixture_offsets[0] != 0)
+        return "mixture_offsets[0] must be 0";
+    for (uint32_t m = 0; m < ms.n_mixtures; ++m)
+        if (ms.mixture_offsets[m + 1] < ms.mixture_offsets[m])
+            return "mixture_offsets must be non-decreasing";
+    const uint32_t nEntries = ms.mixture_offsets[ms.n_mixtures];
+    for (uint32_t e = 0; e < nEntries; ++e)
+        if (ms.mixture_densities[e] >= ms.n_densities)
+            return "mixture entry references a density out of range";
+    for (uint32_t i = 0; i < ms.n_densities; ++i) {
+        if (ms.density_mean[i] >= ms.n_means)
+            return "density references a mean out of range";
+        if (ms.density_covariance[i] >= ms.n_covariances)
+            return "density references a covariance out of range";
+    }
+    // require(checkDiagonal(diagonal)) -- CovarianceFeatureScorerElement.cc:26,38-42
+    for (size_t i = 0; i < static_cast<size_t>(ms.n_covariances) * ms.dimension; ++i)
+        if (!(ms.variances[i] > 0))
+            return "covariance diagonal must be > 0";
+    return "";
+}
+
+static void buildTiling(const gmm_mixture_set& ms, ShardRange shard, Tiling& t) {
+    const uint32_t nMix = shard.end - shard.begin;
+    t.mixTileOffset.assign(nMix + 1, 0);
+    t.tileCovariance.clear();
+    t.rowEntry.clear();
+    t.rowDensityInMixture.clear();
+    t.maxEntriesPerMixture = 0;
+    std::vector<uint32_t> order;
+    for (uint32_t mi = 0; mi < nMix; ++mi) {
+        const uint32_t m = shard.begin + mi;
+        const uint32_t b = ms.mixture_offsets[m], e = ms.mixture_offsets[m + 1];
+        t.maxEntriesPerMixture = std::max(t.maxEntriesPerMixture, e - b);
+        order.resize(e - b);
+        std::iota(order.begin(), order.end(), b);
+        // group rows by covariance (one frame-side operand per tile); stable keeps entry order
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+            return ms.density_covariance[ms.mixture_densities[x]] < ms.density_covariance[ms.mixture_densities[y]];
+        });
+        size_t i = 0;
+        while (i < order.size()) {
+            const uint32_t cov = ms.density_covariance[ms.mixture_densities[order[i]]];
+            size_t         j   = i;
+            while (j < order.size() && ms.density_covariance[ms.mixture_densities[order[j]]] == cov)
+                ++j;
+            for (size_t r0 = i; r0 < j; r0 += kTileRows) {
+                t.tileCovariance.push_back(cov);
+                for (uint32_t r = 0; r < kTileRows; ++r) {
+                    if (r0 + r < j) {
+                        t.rowEntry.push_back(order[r0 + r]);
+                        t.rowDensityInMixture.push_back(order[r0 + r] - b);
+                    }
+                    else {
+                        t.rowEntry.push_back(UINT32_MAX);
+                        t.rowDensityInMixture.push_back(UINT32_MAX);
+                    }
+                }
+            }
+            i = j;
+        }
+        t.mixTileOffset[mi + 1] = static_cast<uint32_t>(t.tileCovariance.size());
+    }
+    t.nTiles = static_cast<uint32_t>(t.tileCovariance.size());
+}
+
+static ShardRange normalizeShard(const gmm_mixture_set& ms, ShardRange s) {
+    if (s.begin == 0 && s.end == 0)
+        return ShardRange{0, ms.n_mixtures};
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// quantized scorers: SIMD-diagonal-maximum, batch-diagonal-maximum-int
+// ---------------------------------------------------------------------------
+
+std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out) {
+    std::string err = validate(ms);
+    if (!err.empty())
+        return err;
+    shard = normalizeShard(ms, shard);
+    if (shard.begin > shard.end || shard.end > ms.n_mixtures)
+        return "invalid mixture shard";
+    const uint32_t D = ms.dimension, C = ms.n_covariances;
+    if (flavor == Flavor::BatchInt && C != 1)
+        return "feature scorer supports only globally pooled variance";  // BatchFeatureScorer.cc:341-343
+    if (D > 2 * kI8K)
+        return "quantized scorer supports dimension <= 128";
+    out            = PreparedQuantized();
+    out.flavor     = flavor;
+    out.dimension  = D;
+    out.paddedDimension = (D + 15u) / 16u * 16u;  // IntelOptimization.hh:51-58 (BlockSize 16)
+    out.nCovariances = C;
+    out.nMixtures  = shard.end - shard.begin;
+    out.kSteps     = (D + kI8K - 1) / kI8K;
+
+    // CovarianceFeatureScorerElement::operator= (CovarianceFeatureScorerElement.cc:20-36)
+    std::vector<float> isv(static_cast<size_t>(C) * D);
+    std::vector<float> logNorm(C);
+    for (uint32_t c = 0; c < C; ++c) {
+        const float* var = ms.variances + static_cast<size_t>(c) * D;
+        for (uint32_t k = 0; k < D; ++k)
+            isv[static_cast<size_t>(c) * D + k] = refInverseSqrt(var[k]);
+        logNorm[c] = static_cast<float>(refGaussLogNorm(var, D));
+    }
+
+    // getScaling (SimdFeatureScorer.cc:106-126) / quantizationScale (BatchFeatureScorer.cc:318-336):
+    // bounds of mean * isv over ALL densities of the mixture set (shards share one scale).
+    float minMean = FLT_MAX, maxMean = -FLT_MAX;
+    for (uint32_t i = 0; i < ms.n_densities; ++i) {
+        const float* mean = ms.means + static_cast<size_t>(ms.density_mean[i]) * D;
+        const float* iv   = isv.data() + static_cast<size_t>(ms.density_covariance[i]) * D;
+        for (uint32_t k = 0; k < D; ++k) {
+            float dm = mean[k] * iv[k];
+            minMean  = std::min(minMean, dm);
+            maxMean  = std::max(maxMean, dm);
+        }
+    }
+    const float s             = refQuantizationScalingFactor(minMean, maxMean);
+    out.scaling               = s;
+    out.scalingSquared        = s * s;                         // cc:72
+    out.inverseQuantizationFactor = 0.5f / out.scalingSquared; // cc:73
+    out.batchScale            = static_cast<float>(2.0 * static_cast<double>(out.scalingSquared));  // cc:356
+
+    // scale(s): isv *= s; logNorm *= s*s  (CovarianceFeatureScorerElement.cc:45-51, BatchFeatureScorer.cc:357-359)
+    out.isvScaled.resize(isv.size());
+    out.logNormScaled.resize(C);
+    for (uint32_t c = 0; c < C; ++c) {
+        for (uint32_t k = 0; k < D; ++k)
+            out.isvScaled[static_cast<size_t>(c) * D + k] = isv[static_cast<size_t>(c) * D + k] * s;
+        out.logNormScaled[c] = logNorm[c] * (s * s);
+    }
+
+    // reference tables per mixture entry: prepared mean (u8, 0-padded to Dp) and constant weight
+    const uint32_t nEntries = ms.mixture_offsets[ms.n_mixtures];
+    const uint32_t Dp       = out.paddedDimension;
+    out.preparedMean.assign(static_cast<size_t>(nEntries) * Dp, 0);
+    out.constantWeight.assign(nEntries, 0);
+    for (uint32_t m = 0; m < ms.n_mixtures; ++m) {
+        for (uint32_t e = ms.mixture_offsets[m]; e < ms.mixture_offsets[m + 1]; ++e) {
+            const uint32_t dns  = ms.mixture_densities[e];
+            const uint32_t cov  = ms.density_covariance[dns];
+            const float*   mean = ms.means + static_cast<size_t>(ms.density_mean[dns]) * D;
+            const float*   iv   = out.isvScaled.data() + static_cast<size_t>(cov) * D;
+            for (uint32_t k = 0; k < D; ++k)
+                out.preparedMean[static_cast<size_t>(e) * Dp + k] = refQuantize(mean[k] * iv[k]);
+            const double lw = ms.mixture_log_weights[e];
+            if (flavor == Flavor::Simd) {
+                // SimdFeatureScorer.cc:96 + IntelOptimization.cc:47
+                float w = static_cast<float>(static_cast<double>(out.scalingSquared * -2.0f) * lw);
+                out.constantWeight[e] = refTruncF32(w + out.logNormScaled[cov]);
+            }
+            else {
+                // BatchFeatureScorer.cc:376 (logNormFactor = logNorm * scaleSquared, cc:359)
+                out.constantWeight[e] = refTruncF64(static_cast<double>(out.logNormScaled[cov]) -
+                                                    static_cast<double>(out.batchScale) * lw);
+            }
+        }
+    }
+
+    // device tiles
+    buildTiling(ms, shard, out.tiling);
+    uint32_t ib = 1;
+    while ((1u << ib) < std::max<uint32_t>(out.tiling.maxEntriesPerMixture, 2u))
+        ++ib;
+    out.idxBits = ib;
+    // packed = value * 2^ib + density must stay below the padding-row value.  With several
+    // covariances the kernel adds the frame's sum (q-128)^2 << ib (<= D * 128^2) to every row,
+    // padding rows included, so their constant leaves that much headroom.
+    const uint32_t T      = out.tiling.nTiles;
+    const uint32_t KS     = out.kSteps;
+    const bool     multiC = C > 1;
+    const int64_t  ssMax  = multiC ? static_cast<int64_t>(D) * 128 * 128 : 0;
+    const int64_t  packedLimit = (static_cast<int64_t>(1) << (31 - ib)) - 2 - ssMax;
+    if (packedLimit <= 0)
+        return "mixtures too large for the packed (score, density) int32 encoding";
+    const int32_t padRow = static_cast<int32_t>(static_cast<int64_t>(kPadRowPacked) - (ssMax << ib));
+    out.tileA.assign(static_cast<size_t>(T) * KS * kLanes * 16, 0);
+    out.tileP.assign(static_cast<size_t>(T) * kTileRows, padRow);
+    for (uint32_t t = 0; t < T; ++t) {
+        for (uint32_t r = 0; r < kTileRows; ++r) {
+            const uint32_t e = out.tiling.rowEntry[static_cast<size_t>(t) * kTileRows + r];
+            if (e == UINT32_MAX)
+                continue;
+            const uint8_t* pm     = out.preparedMean.data() + static_cast<size_t>(e) * Dp;
+            int64_t        sumSq  = 0;
+            int64_t        sumAbs = 0;
+            for (uint32_t k = 0; k < D; ++k) {
+                const int32_t an = 128 - static_cast<int32_t>(pm[k]);  // -(a - 128)
+                sumSq += static_cast<int64_t>(an) * an;
+                sumAbs += an < 0 ? -an : an;
+                if (an < -128 || an > 127)
+                    return "prepared mean outside the s8 operand range (mean quantized to 0)";
+                // fragment order: k = ks*64 + 16*(lane>>4) + j, row = lane & 15
+                const uint32_t ks = k / kI8K, kk = k % kI8K;
+                const uint32_t lane = (kk / 16) * 16 + r, j = kk % 16;
+                out.tileA[((static_cast<size_t>(t) * KS + ks) * kLanes + lane) * 16 + j] = static_cast<int8_t>(an);
+            }
+            const int64_t biasv = static_cast<int64_t>(out.constantWeight[e]) + sumSq;
+            const int64_t bound = (biasv < 0 ? -biasv : biasv) + 2 * 128 * sumAbs + ssMax;
+            if (bound > packedLimit)
+                return "model outside the packed (score, density) int32 range; use fewer densities per mixture";
+            const uint32_t dnsIdx = out.tiling.rowDensityInMixture[static_cast<size_t>(t) * kTileRows + r];
+            out.tileP[static_cast<size_t>(t) * kTileRows + r] =
+                    static_cast<int32_t>(biasv * (static_cast<int64_t>(1) << ib) + dnsIdx);
+        }
+    }
+    out.isvDevice.assign(static_cast<size_t>(C) * KS * kI8K, 0.0f);
+    for (uint32_t c = 0; c < C; ++c)
+        for (uint32_t k = 0; k < D; ++k)
+            out.isvDevice[static_cast<size_t>(c) * KS * kI8K + k] = out.isvScaled[static_cast<size_t>(c) * D + k];
+    return "";
+}
+
+// ---------------------------------------------------------------------------
+// float scorers: diagonal-maximum, batch-diagonal-maximum-float
+// ---------------------------------------------------------------------------
+
+std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
+                         ShardRange shard, PreparedFloat& out) {
+    std::string err = validate(ms);
+    if (!err.empty())
+        return err;
+    shard = normalizeShard(ms, shard);
+    if (shard.begin > shard.end || shard.end > ms.n_mixtures)
+        return "invalid mixture shard";
+    const uint32_t D = ms.dimension, C = ms.n_covariances;
+    if (flavor == Flavor::BatchFloat && C != 1)
+        return "feature scorer supports only globally pooled covariance";  // BatchFeatureScorer.cc:146-148
+    if (D > 126)
+        return "float scorer supports dimension <= 126";
+    out              = PreparedFloat();
+    out.flavor       = flavor;
+    out.dimension    = D;
+    out.nCovariances = C;
+    out.nMixtures    = shard.end - shard.begin;
+    out.foldNorm     = C > 1;
+    const uint32_t kUsed = D + 1 + (out.foldNorm ? 1 : 0);
+    out.kSteps       = f32KStepsInstantiated((kUsed + 3) / 4);
+
+    // diagonal-maximum: covariance.scale(gaussianScale_ = sqrt(gaussian-scale)) (GDMFS.cc:51,83-84);
+    // batch-float: unscaled (BatchFeatureScorer.cc:155-160).
+    const bool  dm = flavor == Flavor::DiagonalMaximum;
+    const float gs = dm ? static_cast<float>(std::sqrt(static_cast<double>(gaussianScale))) : 1.0f;
+    out.isv.resize(static_cast<size_t>(C) * D);
+    out.logNorm.resize(C);
+    for (uint32_t c = 0; c < C; ++c) {
+        const float* var = ms.variances + static_cast<size_t>(c) * D;
+        for (uint32_t k = 0; k < D; ++k) {
+            float iv = refInverseSqrt(var[k]);
+            out.isv[static_cast<size_t>(c) * D + k] = dm ? iv * gs : iv;
+        }
+        float ln      = static_cast<float>(refGaussLogNorm(var, D));
+        out.logNorm[c] = dm ? ln * (gs * gs) : ln;
+    }
+
+    buildTiling(ms, shard, out.tiling);
+    const uint32_t T = out.tiling.nTiles, KS = out.kSteps;
+    out.tileA.assign(static_cast<size_t>(T) * KS * kLanes, 0.0f);
+    std::vector<float> row(KS * 4);
+    for (uint32_t t = 0; t < T; ++t) {
+        for (uint32_t r = 0; r < kTileRows; ++r) {
+            const uint32_t e = out.tiling.rowEntry[static_cast<size_t>(t) * kTileRows + r];
+            std::fill(row.begin(), row.end(), 0.0f);
+            if (e == UINT32_MAX) {
+                row[D] = FLT_MAX;  // padding row: bias +FLT_MAX never wins a strict minimum
+            }
+            else {
+                const uint32_t dns  = ms.mixture_densities[e];
+                const uint32_t cov  = ms.density_covariance[dns];
+                const float*   mean = ms.means + static_cast<size_t>(ms.density_mean[dns]) * D;
+                const float*   iv   = out.isv.data() + static_cast<size_t>(cov) * D;
+                double         mm   = 0;
+                for (uint32_t k = 0; k < D; ++k) {
+                    const float mp = mean[k] * iv[k];
+                    row[k]         = -2.0f * mp;
+                    mm += static_cast<double>(mp) * mp;
+                }
+                double c;
+                if (dm) {
+                    // minus2LogWeights_ (MixtureFeatureScorerElement.cc:26,30-33) + logNorm (GDMFS.cc:126-129)
+                    const float m2lw = static_cast<float>(-2 * ms.mixture_log_weights[e]) * mixtureWeightScale;
+                    c = static_cast<double>(m2lw) + static_cast<double>(out.logNorm[cov]);
+                }
+                else {
+                    // BatchFeatureScorer.cc:167: constants = logNormFactor - 2 * logWeight (f32)
+                    c = static_cast<float>(static_cast<double>(out.logNorm[cov]) - 2 * ms.mixture_log_weights[e]);
+                }
+                row[D] = static_cast<float>(mm + c);
+                if (out.foldNorm)
+                    row[D + 1] = 1.0f;
+            }
+            // fragment order of v_mfma_f32_16x16x4_f32: lane = 16*(k&3) + row, step s = k>>2
+            for (uint32_t k = 0; k < KS * 4; ++k)
+                out.tileA[(static_cast<size_t>(t) * KS + k / 4) * kLanes + (k % 4) * 16 + r] = row[k];
+        }
+    }
+    out.isvDevice.assign(static_cast<size_t>(C) * KS * 4, 0.0f);
+    for (uint32_t c = 0; c < C; ++c)
+        for (uint32_t k = 0; k < D; ++k)
+            out.isvDevice[static_cast<size_t>(c) * KS * 4 + k] = out.isv[static_cast<size_t>(c) * D + k];
+    return "";
+}
+
+}  // namespace rasr_gmm

@@ -1,0 +1,102 @@
+// gmm_prepare.hh -- host-side model preparation for the MI355X GMM scorer.
+//
+// The reference scorers prepare their tables on the host once per model
+// (SimdFeatureScorer.cc:64-104, GaussDiagonalMaximumFeatureScorer.cc:64-86,
+// BatchFeatureScorer.cc:145-172,339-380).  This file reproduces that arithmetic
+// bit for bit (independently of the compiler flags this file is built with) and
+// lays the result out for the device kernels:
+//
+//   * densities of a mixture are grouped by covariance and cut into tiles of 16
+//     rows (one MFMA row block); tiles of a mixture are contiguous (CSR
+//     mixture -> tiles), the tail of every tile is padded with rows that can
+//     never win the minimum;
+//   * quantized mode (SIMD-diagonal-maximum, batch-int): per tile a 1 KiB s8
+//     operand block in v_mfma_i32_16x16x64_i8 fragment order plus 16 packed
+//     int32 row constants;
+//   * float mode (diagonal-maximum, batch-float): per tile K/4 x 64 f32 operands
+//     in v_mfma_f32_16x16x4_f32 fragment order, the row constant folded into
+//     the K column `dimension`.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/rasr_gmm.h"
+
+namespace rasr_gmm {
+
+constexpr uint32_t kTileRows     = 16;   // densities per MFMA tile
+constexpr uint32_t kLanes        = 64;   // wavefront
+constexpr uint32_t kI8K          = 64;   // K of v_mfma_i32_16x16x64_i8
+constexpr int32_t  kPadRowPacked = 0x7fffffff;
+
+// K/4 steps of the float kernel that are instantiated (gmm_kernels.hip); a model is padded up to one of these.
+inline uint32_t f32KStepsInstantiated(uint32_t kSteps) {
+    static const uint32_t ks[] = {2, 4, 6, 8, 10, 12, 14, 16, 20, 24, 28, 32};
+    for (uint32_t k : ks)
+        if (kSteps <= k)
+            return k;
+    return 0;
+}
+
+// ---- reference scalar arithmetic (flag-independent restatement) ----
+float   refInverseSqrt(float x);               // Utilities.hh:87-91 as built (-ffast-math): rsqrtss + NR
+int32_t refRoundToInt(float x);                // (int)round(x) as built: add 0.49999997 with sign, cvttss2si
+uint8_t refQuantize(float x);                  // quantize<f32,u8>, Utilities.hh:179-191
+double  refGaussLogNorm(const float* var, uint32_t d);   // Utilities.hh:55-76
+float   refQuantizationScalingFactor(float minv, float maxv); // SimdFeatureScorer.cc:128-133 as built
+int32_t refTruncF32(float x);                  // (s32)float, cvttss2si
+int32_t refTruncF64(double x);                 // (s32)double, cvttsd2si
+
+enum class Flavor : int { Simd = 0, BatchInt = 1, DiagonalMaximum = 2, BatchFloat = 3 };
+
+struct Tiling {
+    uint32_t              nTiles = 0;
+    std::vector<uint32_t> mixTileOffset;   // [nMixtures+1] (shard-relative mixtures)
+    std::vector<uint32_t> tileCovariance;  // [nTiles]
+    std::vector<uint32_t> rowEntry;        // [nTiles*16] entry index or UINT32_MAX for padding
+    std::vector<uint32_t> rowDensityInMixture; // [nTiles*16]
+    uint32_t              maxEntriesPerMixture = 0;
+};
+
+struct PreparedQuantized {
+    Flavor   flavor = Flavor::Simd;
+    uint32_t dimension = 0, paddedDimension = 0, nCovariances = 0, nMixtures = 0;
+    uint32_t kSteps = 1;              // K blocks of 64
+    uint32_t idxBits = 1;
+    float    scaling = 0, scalingSquared = 0, inverseQuantizationFactor = 0;
+    float    batchScale = 0;          // BatchIntFeatureScorer::scale_ = 2 s^2
+    std::vector<float>   isvScaled;   // [C][dimension]
+    std::vector<float>   logNormScaled; // [C]
+    std::vector<uint8_t> preparedMean;  // [entries][paddedDimension]  (reference table, for inspection)
+    std::vector<int32_t> constantWeight;// [entries]
+    Tiling               tiling;
+    std::vector<int8_t>  tileA;       // [nTiles][kSteps][64 lanes][16]
+    std::vector<int32_t> tileP;       // [nTiles][16]
+    std::vector<float>   isvDevice;   // [C][kSteps*64], zero padded
+};
+
+struct PreparedFloat {
+    Flavor   flavor = Flavor::DiagonalMaximum;
+    uint32_t dimension = 0, nCovariances = 0, nMixtures = 0;
+    uint32_t kSteps = 0;              // K/4
+    bool     foldNorm = false;        // multi-covariance: ||x'||^2 folded into K column dimension+1
+    std::vector<float> isv;           // [C][dimension] (after gaussian-scale)
+    std::vector<float> logNorm;       // [C]
+    Tiling             tiling;
+    std::vector<float> tileA;         // [nTiles][kSteps][64 lanes]
+    std::vector<float> isvDevice;     // [C][kSteps*4] zero padded
+};
+
+struct ShardRange {
+    uint32_t begin = 0, end = 0;
+};
+
+// Returns empty string on success, else an error message.
+std::string validate(const gmm_mixture_set& ms);
+std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out);
+std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
+                         ShardRange shard, PreparedFloat& out);
+
+}  // namespace rasr_gmm

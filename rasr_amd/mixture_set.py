@@ -1,0 +1,146 @@
+"""In-memory mixture set (the data of Mm::MixtureSet, src/Mm/MixtureSet.hh:140-212)
+and synthetic models of the shape SURVEY.md section 8(d) benchmarks on.
+
+A MixtureSet holds numpy arrays; `desc()` returns the ctypes descriptor of
+include/rasr_gmm.h (gmm_mixture_set) pointing into them (keep the MixtureSet
+alive while the descriptor is used).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _capi
+
+
+@dataclass
+class MixtureSet:
+    means: np.ndarray                # [n_means, D] f32
+    variances: np.ndarray            # [n_covariances, D] f32 (Covariance::diagonal())
+    density_mean: np.ndarray         # [n_densities] u32
+    density_covariance: np.ndarray   # [n_densities] u32
+    mixture_offsets: np.ndarray      # [n_mixtures + 1] u32
+    mixture_densities: np.ndarray    # [n_entries] u32
+    mixture_log_weights: np.ndarray  # [n_entries] f64 (Mm::Weight)
+    _keep: list = field(default_factory=list, repr=False)
+
+    def __post_init__(self):
+        self.means = np.ascontiguousarray(self.means, dtype=np.float32)
+        self.variances = np.ascontiguousarray(self.variances, dtype=np.float32)
+        self.density_mean = np.ascontiguousarray(self.density_mean, dtype=np.uint32)
+        self.density_covariance = np.ascontiguousarray(self.density_covariance, dtype=np.uint32)
+        self.mixture_offsets = np.ascontiguousarray(self.mixture_offsets, dtype=np.uint32)
+        self.mixture_densities = np.ascontiguousarray(self.mixture_densities, dtype=np.uint32)
+        self.mixture_log_weights = np.ascontiguousarray(self.mixture_log_weights, dtype=np.float64)
+
+    @property
+    def dimension(self) -> int:
+        return int(self.means.shape[1])
+
+    @property
+    def n_mixtures(self) -> int:
+        return int(self.mixture_offsets.shape[0] - 1)
+
+    @property
+    def n_densities(self) -> int:
+        return int(self.density_mean.shape[0])
+
+    @property
+    def n_entries(self) -> int:
+        return int(self.mixture_offsets[-1])
+
+    @property
+    def n_covariances(self) -> int:
+        return int(self.variances.shape[0])
+
+    def desc(self) -> _capi.MixtureSetDesc:
+        def p(a, t):
+            return a.ctypes.data_as(ctypes.POINTER(t))
+        d = _capi.MixtureSetDesc()
+        d.dimension = self.dimension
+        d.n_means = self.means.shape[0]
+        d.means = p(self.means, ctypes.c_float)
+        d.n_covariances = self.n_covariances
+        d.variances = p(self.variances, ctypes.c_float)
+        d.n_densities = self.n_densities
+        d.density_mean = p(self.density_mean, ctypes.c_uint32)
+        d.density_covariance = p(self.density_covariance, ctypes.c_uint32)
+        d.n_mixtures = self.n_mixtures
+        d.mixture_offsets = p(self.mixture_offsets, ctypes.c_uint32)
+        d.mixture_densities = p(self.mixture_densities, ctypes.c_uint32)
+        d.mixture_log_weights = p(self.mixture_log_weights, ctypes.c_double)
+        return d
+
+    def save_npz(self, path: str) -> None:
+        np.savez_compressed(path, means=self.means, variances=self.variances, density_mean=self.density_mean,
+                            density_covariance=self.density_covariance, mixture_offsets=self.mixture_offsets,
+                            mixture_densities=self.mixture_densities, mixture_log_weights=self.mixture_log_weights)
+
+    @staticmethod
+    def load_npz(path: str) -> "MixtureSet":
+        z = np.load(path, allow_pickle=False)
+        return MixtureSet(z["means"], z["variances"], z["density_mean"], z["density_covariance"],
+                          z["mixture_offsets"], z["mixture_densities"], z["mixture_log_weights"])
+
+
+def synthetic_mixture_set(n_mixtures: int, densities_per_mixture, dimension: int, seed: int = 1234,
+                          n_covariances: int = 1, weights: str = "uniform") -> MixtureSet:
+    """SURVEY.md section 8(d) synthetic model.
+
+    pooled variance  s2_k = 0.5 + |N(0,1)|;  means ~ N(0,1);  one mean per density;
+    weights: "uniform" -> log(1/K_m);  "random" -> normalized Dirichlet(1) draws.
+    densities_per_mixture: int, or a sequence of per-mixture counts (ragged models).
+    n_covariances > 1 assigns every density a random covariance (untied variant).
+    """
+    rng = np.random.Generator(np.random.PCG64(seed))
+    if np.isscalar(densities_per_mixture):
+        counts = np.full(n_mixtures, int(densities_per_mixture), dtype=np.int64)
+    else:
+        counts = np.asarray(densities_per_mixture, dtype=np.int64)
+        assert counts.shape[0] == n_mixtures
+    n = int(counts.sum())
+    variances = (0.5 + np.abs(rng.standard_normal((n_covariances, dimension), dtype=np.float32))).astype(np.float32)
+    means = rng.standard_normal((n, dimension), dtype=np.float32)
+    offsets = np.zeros(n_mixtures + 1, dtype=np.uint32)
+    offsets[1:] = np.cumsum(counts)
+    if n_covariances == 1:
+        dcov = np.zeros(n, dtype=np.uint32)
+    else:
+        dcov = rng.integers(0, n_covariances, size=n, dtype=np.uint32)
+    if weights == "uniform":
+        logw = np.concatenate([np.full(c, np.log(1.0 / c)) for c in counts]) if n else np.zeros(0)
+    elif weights == "random":
+        parts = []
+        for c in counts:
+            w = rng.exponential(1.0, size=int(c))
+            parts.append(np.log(w / w.sum()))
+        logw = np.concatenate(parts) if parts else np.zeros(0)
+    else:
+        raise ValueError(weights)
+    return MixtureSet(means=means, variances=variances, density_mean=np.arange(n, dtype=np.uint32),
+                      density_covariance=dcov, mixture_offsets=offsets,
+                      mixture_densities=np.arange(n, dtype=np.uint32), mixture_log_weights=logw)
+
+
+def synthetic_frames(n_frames: int, dimension: int, seed: int = 4321) -> np.ndarray:
+    """Feature vectors x ~ N(0,1), [n_frames, D] f32."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return rng.standard_normal((n_frames, dimension), dtype=np.float32)
+
+
+def ragged_counts(n_mixtures: int, total: int, low: int = 64, high: int = 256, seed: int = 99) -> np.ndarray:
+    """K_m ~ U[low, high] rescaled so that sum K_m == total (SURVEY.md 8(d) ragged variant)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = rng.integers(low, high + 1, size=n_mixtures).astype(np.float64)
+    k = np.maximum(1, np.round(k * total / k.sum())).astype(np.int64)
+    diff = total - int(k.sum())
+    i = 0
+    while diff != 0:
+        step = 1 if diff > 0 else -1
+        if k[i % n_mixtures] + step >= 1:
+            k[i % n_mixtures] += step
+            diff -= step
+        i += 1
+    return k

@@ -1,0 +1,139 @@
+"""Python handle over the C-ABI scorer (include/rasr_gmm.h).
+
+Used by the tests and bench.py; RASR itself binds the C-ABI from C++
+(rasr_amd/csrc/host/GpuFeatureScorer.hh).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _capi
+from .mixture_set import MixtureSet
+
+
+def _type_id(t) -> int:
+    if isinstance(t, str):
+        return _capi.SCORER_TYPES[t]
+    return int(t)
+
+
+def default_config() -> _capi.ScorerConfig:
+    cfg = _capi.ScorerConfig()
+    _capi.load_library().gmm_default_config(ctypes.byref(cfg))
+    return cfg
+
+
+class Scorer:
+    """One prepared model resident on one GPU (gmm_scorer_create)."""
+
+    def __init__(self, mixture_set: MixtureSet, scorer_type="SIMD-diagonal-maximum", max_frames: int = 4096,
+                 device: int = 0, mixture_weight_scale: float = 1.0, gaussian_scale: float = 1.0,
+                 score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None):
+        self._lib = _capi.load_library()
+        self.mixture_set = mixture_set
+        self.type = _type_id(scorer_type)
+        cfg = default_config()
+        cfg.max_frames = int(max_frames)
+        cfg.mixture_weight_scale = mixture_weight_scale
+        cfg.gaussian_scale = gaussian_scale
+        cfg.score_scale = score_scale
+        if mixture_range is not None:
+            cfg.mixture_begin, cfg.mixture_end = int(mixture_range[0]), int(mixture_range[1])
+        self.max_frames = int(max_frames)
+        self._desc = mixture_set.desc()
+        h = ctypes.c_void_p()
+        _capi.check(self._lib.gmm_scorer_create(ctypes.byref(self._desc), self.type, ctypes.byref(cfg), int(device),
+                                                ctypes.byref(h)), "gmm_scorer_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.gmm_scorer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def n_mixtures(self) -> int:
+        return int(self._lib.gmm_scorer_n_mixtures(self._h))
+
+    def dimension(self) -> int:
+        return int(self._lib.gmm_scorer_dimension(self._h))
+
+    def score_device(self, frames, scores, best=None, stream=None, n_frames=None) -> None:
+        """frames: torch cuda f32 [F, >=D] (row stride = frames.stride(0)); scores: [M, >=F] f32;
+        best: [M, >=F] int32/uint32 or None.  Asynchronous on `stream` (torch stream or raw handle)."""
+        f = int(frames.shape[0] if n_frames is None else n_frames)
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device)
+        s = getattr(stream, "cuda_stream", stream)
+        rc = self._lib.gmm_score_device(self._h, ctypes.c_void_p(frames.data_ptr()), f, int(frames.stride(0)),
+                                        ctypes.c_void_p(scores.data_ptr()),
+                                        ctypes.c_void_p(best.data_ptr()) if best is not None else None,
+                                        int(scores.stride(0)), ctypes.c_void_p(s) if s else None)
+        _capi.check(rc, "gmm_score_device")
+
+    def score_host(self, frames: np.ndarray, want_best: bool = True):
+        frames = np.ascontiguousarray(frames, dtype=np.float32)
+        f = frames.shape[0]
+        m = self.n_mixtures()
+        scores = np.empty((m, f), dtype=np.float32)
+        best = np.empty((m, f), dtype=np.uint32) if want_best else None
+        rc = self._lib.gmm_score_host(self._h, frames.ctypes.data_as(ctypes.c_void_p), f, frames.shape[1],
+                                      scores.ctypes.data_as(ctypes.c_void_p),
+                                      best.ctypes.data_as(ctypes.c_void_p) if best is not None else None, f)
+        _capi.check(rc, "gmm_score_host")
+        return scores, best
+
+    def set_timing(self, enable: bool) -> None:
+        _capi.check(self._lib.gmm_scorer_set_timing(self._h, int(bool(enable))), "gmm_scorer_set_timing")
+
+    def kernel_time(self, reset: bool = True):
+        """(total ms, launches) of the scorer kernel since the last reset (HIP events on its stream)."""
+        ms, n = ctypes.c_double(), ctypes.c_uint32()
+        _capi.check(self._lib.gmm_scorer_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n), int(reset)),
+                    "gmm_scorer_kernel_time")
+        return ms.value, n.value
+
+    def quantization(self):
+        s, q = ctypes.c_float(), ctypes.c_float()
+        _capi.check(self._lib.gmm_scorer_quantization(self._h, ctypes.byref(s), ctypes.byref(q)),
+                    "gmm_scorer_quantization")
+        return s.value, q.value
+
+    def multiply_and_quantize(self, feature: np.ndarray) -> np.ndarray:
+        feature = np.ascontiguousarray(feature, dtype=np.float32)
+        dp = (self.dimension() + 15) // 16 * 16
+        out = np.empty((self.mixture_set.n_covariances, dp), dtype=np.uint8)
+        _capi.check(self._lib.gmm_scorer_multiply_and_quantize(self._h, feature.ctypes.data_as(ctypes.c_void_p),
+                                                               out.ctypes.data_as(ctypes.c_void_p)),
+                    "gmm_scorer_multiply_and_quantize")
+        return out
+
+
+def prepare_quantized_host(ms: MixtureSet, scorer_type="SIMD-diagonal-maximum") -> dict:
+    """Host-side prepared tables of the quantized scorers (no GPU needed)."""
+    lib = _capi.load_library()
+    d = ms.desc()
+    dp = (ms.dimension + 15) // 16 * 16
+    s = ctypes.c_float()
+    isv = np.empty((ms.n_covariances, ms.dimension), dtype=np.float32)
+    ln = np.empty(ms.n_covariances, dtype=np.float32)
+    pm = np.empty((ms.n_entries, dp), dtype=np.uint8)
+    cw = np.empty(ms.n_entries, dtype=np.int32)
+    _capi.check(lib.gmm_prepare_quantized_host(ctypes.byref(d), _type_id(scorer_type), ctypes.byref(s),
+                                               isv.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                                               pm.ctypes.data_as(ctypes.c_void_p), cw.ctypes.data_as(ctypes.c_void_p)),
+                "gmm_prepare_quantized_host")
+    return {"scaling": s.value, "isv": isv, "log_norm": ln, "prepared_mean": pm, "constant_weight": cw}

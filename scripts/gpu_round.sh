@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench lines, rocprofv3 kernel-trace summary.
+# Each GPU step has its own time limit; a crash/fault/timeout (rc other than 0/1)
+# stops the script so nothing else touches the GPU after a fault.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -5 $OUT/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"pytest smoke bench_fp32 bench_simd prof"}
+for s in $STEPS; do
+  case $s in
+    pytest) step pytest 1200 python -m pytest tests -x -q -m gpu ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench_fp32) step bench_fp32 600 python bench.py --mode fp32 --steps 20 --warmup 3 ;;
+    bench_simd) step bench_simd 600 python bench.py --mode simd --steps 20 --warmup 3 --cpu-baseline off ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --mode fp32 --steps 10 --warmup 2 --cpu-baseline off --extra-mode ;;
+  esac
+done
+echo done

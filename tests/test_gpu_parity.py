@@ -1,0 +1,237 @@
+"""GPU parity: the MI355X scorer (through the C-ABI) against the CPU restatement.
+
+Tolerances (written here, per the north star):
+  * SIMD-diagonal-maximum, batch-diagonal-maximum-int: BIT-EXACT scores and best densities.
+  * diagonal-maximum, batch-diagonal-maximum-float (fp32 MFMA): |gpu - ref| <= 1e-4 * max(1, |ref|);
+    best density identical wherever the two best candidates differ by more than that tolerance.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import rasr_amd as ra
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-4
+
+
+def _gpu_scores(ms, frames, kind, **kw):
+    sc = ra.Scorer(ms, kind, max_frames=max(len(frames), 1), **kw)
+    return sc.score_host(frames)
+
+
+def _assert_bit_exact(a, b):
+    assert a.shape == b.shape
+    diff = np.flatnonzero(a.view(np.uint32).ravel() != b.view(np.uint32).ravel())
+    assert diff.size == 0, f"{diff.size} scores differ; first {diff[:5]}: {a.ravel()[diff[:5]]} vs {b.ravel()[diff[:5]]}"
+
+
+def _assert_close(gpu, ref):
+    err = np.abs(gpu.astype(np.float64) - ref.astype(np.float64)) / np.maximum(1.0, np.abs(ref.astype(np.float64)))
+    assert err.max() <= REL_TOL, f"max rel err {err.max()}"
+    return err
+
+
+QUANT_CASES = [
+    # (mixtures, densities per mixture (int or 'ragged'), dim, covariances, weights, frames)
+    (100, 10, 39, 1, "uniform", 1000),
+    (37, "ragged", 45, 1, "random", 777),
+    (64, 16, 16, 1, "random", 513),
+    (20, 33, 39, 3, "random", 300),
+    (12, 7, 80, 1, "uniform", 200),
+]
+
+
+def _model(m, k, d, c, w, seed=7):
+    if k == "ragged":
+        k = ra.ragged_counts(m, m * 20, low=1, high=40, seed=seed)
+    return ra.synthetic_mixture_set(m, k, d, seed=seed, n_covariances=c, weights=w)
+
+
+@pytest.mark.parametrize("case", QUANT_CASES)
+def test_simd_diagonal_maximum_bit_exact(gpu, case):
+    m, k, d, c, w, f = case
+    ms = _model(m, k, d, c, w)
+    frames = ra.synthetic_frames(f, d, seed=11)
+    ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames, n_threads=8)
+    s, b = _gpu_scores(ms, frames, "SIMD-diagonal-maximum")
+    _assert_bit_exact(s, ref_s)
+    assert np.array_equal(b, ref_b)
+
+
+@pytest.mark.parametrize("case", [q for q in QUANT_CASES if q[3] == 1])
+def test_batch_int_bit_exact(gpu, case):
+    m, k, d, c, w, f = case
+    ms = _model(m, k, d, c, w)
+    frames = ra.synthetic_frames(f, d, seed=12)
+    ref = oracle.batch_int_score(ms, frames, n_threads=8)
+    s, _ = _gpu_scores(ms, frames, "batch-diagonal-maximum-int")
+    _assert_bit_exact(s, ref)
+
+
+def _check_float(gpu_s, gpu_b, ref_s, ref_b, ms, frames, om):
+    _assert_close(gpu_s, ref_s)
+    if gpu_b is None:
+        return
+    mism = np.argwhere(gpu_b != ref_b)
+    for e, t in mism[:200]:
+        # allowed only for a near tie: both densities score within tolerance in the reference
+        alt = ref_s[e, t]
+        assert abs(float(gpu_s[e, t]) - float(alt)) <= REL_TOL * max(1.0, abs(float(alt)))
+    assert len(mism) <= max(2, 0.001 * gpu_b.size), f"{len(mism)} argmin mismatches"
+
+
+@pytest.mark.parametrize("case", QUANT_CASES)
+def test_diagonal_maximum_fp32(gpu, case):
+    m, k, d, c, w, f = case
+    ms = _model(m, k, d, c, w)
+    frames = ra.synthetic_frames(f, d, seed=13)
+    om = oracle.OracleFloat(ms)
+    ref_s, ref_b = om.score(frames, n_threads=8)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum")
+    _check_float(s, b, ref_s, ref_b, ms, frames, om)
+
+
+def test_diagonal_maximum_scales(gpu):
+    ms = _model(50, 12, 39, 1, "random")
+    frames = ra.synthetic_frames(300, 39, seed=14)
+    ref_s, ref_b = oracle.OracleFloat(ms, mixture_weight_scale=0.7, gaussian_scale=1.3).score(frames, 8)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum", mixture_weight_scale=0.7, gaussian_scale=1.3)
+    _check_float(s, b, ref_s, ref_b, ms, frames, None)
+
+
+@pytest.mark.parametrize("case", [q for q in QUANT_CASES if q[3] == 1])
+def test_batch_float_fp32(gpu, case):
+    m, k, d, c, w, f = case
+    ms = _model(m, k, d, c, w)
+    frames = ra.synthetic_frames(f, d, seed=15)
+    ref = oracle.batch_float_score(ms, frames, n_threads=8)
+    s, _ = _gpu_scores(ms, frames, "batch-diagonal-maximum-float")
+    _assert_close(s, ref)
+
+
+def _edge_model():
+    """Mixtures with 0, 1, 16, 17 densities, duplicated densities (exact ties), shared densities."""
+    rng = np.random.Generator(np.random.PCG64(5))
+    d = 39
+    n = 60
+    means = rng.standard_normal((n, d), dtype=np.float32)
+    means[5] = means[4]  # tie inside mixture
+    var = (0.5 + np.abs(rng.standard_normal((1, d), dtype=np.float32))).astype(np.float32)
+    groups = [[], [0], list(range(1, 17)), list(range(17, 34)), [4, 5, 6], [10, 3, 10, 2], list(range(34, 60))]
+    offs = np.cumsum([0] + [len(g) for g in groups]).astype(np.uint32)
+    dens = np.array([i for g in groups for i in g], dtype=np.uint32)
+    logw = np.concatenate([np.full(len(g), -np.log(max(len(g), 1))) for g in groups])
+    return ra.MixtureSet(means, var, np.arange(n, dtype=np.uint32), np.zeros(n, np.uint32), offs, dens, logw)
+
+
+def test_edge_cases_simd(gpu):
+    ms = _edge_model()
+    frames = ra.synthetic_frames(130, 39, seed=3)
+    frames[0] *= 1000.0   # clipped to 0 / 255 by the quantizer
+    frames[1] = 0.0
+    frames[2] = ms.means[4]  # exact tie between duplicated densities
+    ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+    s, b = _gpu_scores(ms, frames, "SIMD-diagonal-maximum")
+    _assert_bit_exact(s, ref_s)
+    assert np.array_equal(b, ref_b)
+    assert b[0, 0] == 0xFFFFFFFF  # empty mixture: bestDensity = (u32)size_t max
+
+
+def test_edge_cases_float(gpu):
+    ms = _edge_model()
+    frames = ra.synthetic_frames(130, 39, seed=4)
+    frames[0] *= 1000.0
+    frames[2] = ms.means[4]
+    ref_s, ref_b = oracle.OracleFloat(ms).score(frames)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum")
+    assert np.array_equal(s[0], ref_s[0])  # empty mixture: 0.5 * FLT_MAX
+    _check_float(s[1:], b[1:], ref_s[1:], ref_b[1:], ms, frames, None)
+    assert b[4, 2] == 0  # exact tie -> lowest density index (strict '>' in GDMFS.cc:131)
+
+
+def test_single_frame_and_strides(gpu):
+    import torch
+    ms = _model(40, 9, 39, 1, "random")
+    frames = ra.synthetic_frames(70, 39, seed=21)
+    ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+    sc = ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=70)
+    padded = torch.zeros((70, 48), dtype=torch.float32, device=gpu)
+    padded[:, :39] = torch.from_numpy(frames).to(gpu)
+    out = torch.full((40, 80), -1.0, dtype=torch.float32, device=gpu)
+    best = torch.zeros((40, 80), dtype=torch.int32, device=gpu)
+    sc.score_device(padded, out, best)
+    torch.cuda.synchronize()
+    _assert_bit_exact(out[:, :70].cpu().numpy(), ref_s)
+    assert np.array_equal(best[:, :70].cpu().numpy().view(np.uint32), ref_b)
+    assert (out[:, 70:] == -1).all()
+    s1, b1 = sc.score_host(frames[5:6])
+    _assert_bit_exact(s1, ref_s[:, 5:6])
+
+
+def test_score_scale_and_shard(gpu):
+    ms = _model(90, 11, 39, 1, "random")
+    frames = ra.synthetic_frames(100, 39, seed=22)
+    ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+    s, b = _gpu_scores(ms, frames, "SIMD-diagonal-maximum", score_scale=0.25)
+    _assert_bit_exact(s, (np.float32(0.25) * ref_s).astype(np.float32))
+    # mixture shard [30, 75): same quantization scale as the full model
+    sc = ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=100, mixture_range=(30, 75))
+    s2, b2 = sc.score_host(frames)
+    _assert_bit_exact(s2, ref_s[30:75])
+    assert np.array_equal(b2, ref_b[30:75])
+
+
+def test_quantization_accessors(gpu):
+    ms = _model(30, 8, 39, 2, "random")
+    o = oracle.OracleSimd(ms)
+    sc = ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=4)
+    s, q = sc.quantization()
+    assert s == o.scaling and q == o.inverse_quantization_factor
+    x = ra.synthetic_frames(1, 39, seed=9)[0]
+    assert np.array_equal(sc.multiply_and_quantize(x), o.quantize_frame(x))
+
+
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum"])
+def test_full_size_800k_subset(gpu, kind):
+    """BASELINE config 2 model (5000 x 160 densities, D=39): GPU vs oracle on 96 frames."""
+    import torch
+    ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
+    frames = ra.synthetic_frames(96, 39, seed=77)
+    if kind == "SIMD-diagonal-maximum":
+        ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames, n_threads=16)
+    else:
+        ref_s, ref_b = oracle.OracleFloat(ms).score(frames, n_threads=16)
+    s, b = _gpu_scores(ms, frames, kind)
+    if kind == "SIMD-diagonal-maximum":
+        _assert_bit_exact(s, ref_s)
+        assert np.array_equal(b, ref_b)
+    else:
+        _check_float(s, b, ref_s, ref_b, ms, frames, None)
+    del torch
+
+
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum"])
+def test_full_size_batch_invariance(gpu, kind):
+    """At the bench size (8192 frames x 800k densities): scoring the whole batch equals scoring
+    it in uneven pieces, bit for bit (frames are independent; no cross-frame state)."""
+    import torch
+    ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
+    F = 8192
+    frames = torch.from_numpy(ra.synthetic_frames(F, 39, seed=78)).to(gpu)
+    sc = ra.Scorer(ms, kind, max_frames=F)
+    M = sc.n_mixtures()
+    full = torch.empty((M, F), dtype=torch.float32, device=gpu)
+    fullb = torch.empty((M, F), dtype=torch.int32, device=gpu)
+    sc.score_device(frames, full, fullb)
+    part = torch.empty_like(full)
+    partb = torch.empty_like(fullb)
+    cuts = [0, 1, 700, 4096, 5000, F]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        sc.score_device(frames[a:b], part[:, a:b], partb[:, a:b])
+    torch.cuda.synchronize()
+    assert torch.equal(full.view(torch.int32), part.view(torch.int32))
+    assert torch.equal(fullb, partb)
+    assert torch.isfinite(full).all()
+    assert int(fullb.min()) >= 0 and int(fullb.max()) < 160
