@@ -659,3 +659,47 @@ int orc_batch_float_score(const orc_mixture_set* ms, const float* frames, uint32
     free(x.constants);
     return 0;
 }
+
+/* ------------------------------------------------------------------------- */
+/* helpers for known-answer tests                                              */
+/* ------------------------------------------------------------------------- */
+void orc_quantize_array(const float* x, uint32_t n, uint8_t* out) {
+    uint32_t i;
+    for (i = 0; i < n; ++i)
+        out[i] = orc_quantize(x[i]);
+}
+
+/* BatchIntFeatureScorer::init tables (BatchFeatureScorer.cc:339-380): scale_, variance_, constants_ */
+int orc_batch_int_prepare(const orc_mixture_set* ms, float* scale_out, float* variance_out, int32_t* constants_out) {
+    uint32_t k, i, m, D = ms->dimension;
+    float    minMean = FLT_MAX, maxMean = -FLT_MAX, scale, scaleSquared, scale_, logNormFactor;
+    float*   variance;
+    if (ms->n_covariances != 1)
+        return -1;
+    variance = (float*)malloc(sizeof(float) * D);
+    for (k = 0; k < D; ++k)
+        variance[k] = orc_inverse_sqrt(ms->variances[k]);
+    for (i = 0; i < ms->n_densities; ++i) {
+        const float* mean = ms->means + (size_t)ms->density_mean[i] * D;
+        for (k = 0; k < D; ++k) {
+            float dividedMean = mean[k] * variance[k];
+            minMean           = minMean < dividedMean ? minMean : dividedMean;
+            maxMean           = maxMean < dividedMean ? dividedMean : maxMean;
+        }
+    }
+    scale        = orc_quantization_scaling_factor(minMean, maxMean);
+    scaleSquared = scale * scale;
+    scale_       = 2.0 * scaleSquared;
+    for (k = 0; k < D; ++k)
+        variance[k] = variance[k] * scale;
+    logNormFactor = (float)orc_gauss_log_norm(ms->variances, D) * scaleSquared;
+    for (m = 0; m < ms->n_mixtures; ++m) {
+        uint32_t e;
+        for (e = ms->mixture_offsets[m]; e < ms->mixture_offsets[m + 1]; ++e)
+            constants_out[e] = orc_batch_int_constant(logNormFactor, scale_, ms->mixture_log_weights[e]);
+    }
+    *scale_out = scale_;
+    memcpy(variance_out, variance, sizeof(float) * D);
+    free(variance);
+    return 0;
+}

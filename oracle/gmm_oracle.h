@@ -104,6 +104,10 @@ int orc_batch_int_score(const orc_mixture_set* ms, const float* frames, uint32_t
 int orc_batch_float_score(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
                           uint32_t frame_stride, float* scores, int n_threads);
 
+/* ---- helpers for known-answer tests ---- */
+void orc_quantize_array(const float* x, uint32_t n, uint8_t* out);
+int  orc_batch_int_prepare(const orc_mixture_set* ms, float* scale_out, float* variance_out, int32_t* constants_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,8 @@ def load() -> ctypes.CDLL:
         "orc_batch_int_constant": (ctypes.c_int32, [ctypes.c_float, ctypes.c_float, ctypes.c_double]),
         "orc_batch_int_final_score": (ctypes.c_float, [ctypes.c_int32, ctypes.c_float]),
         "orc_float_distance": (ctypes.c_float, [_f32p, _f32p, _f32p, ctypes.c_uint32]),
+        "orc_quantize_array": (None, [_vp, ctypes.c_uint32, _vp]),
+        "orc_batch_int_prepare": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _f32p, _vp, _vp]),
         "orc_simd_prepare": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), ctypes.POINTER(OrcSimdModel)]),
         "orc_simd_free": (None, [ctypes.POINTER(OrcSimdModel)]),
         "orc_simd_quantize_frame": (None, [ctypes.POINTER(OrcSimdModel), _f32p, _vp]),
@@ -250,3 +252,22 @@ def float_distance(feature, mean, isv) -> float:
     i = np.ascontiguousarray(isv, np.float32)
     return load().orc_float_distance(f.ctypes.data_as(_f32p), m.ctypes.data_as(_f32p), i.ctypes.data_as(_f32p),
                                      f.shape[0])
+
+
+def quantize_array(x) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    out = np.empty(x.shape[0], dtype=np.uint8)
+    load().orc_quantize_array(x.ctypes.data_as(_vp), x.shape[0], out.ctypes.data_as(_vp))
+    return out
+
+
+def batch_int_prepare(ms):
+    """(scale_, variance_ [D], constants_ [entries]) of BatchIntFeatureScorer::init."""
+    d = _Desc(ms)
+    scale = ctypes.c_float()
+    var = np.empty(ms.means.shape[1], np.float32)
+    const = np.empty(d.n_entries, np.int32)
+    if load().orc_batch_int_prepare(ctypes.byref(d.c), ctypes.byref(scale), var.ctypes.data_as(_vp),
+                                    const.ctypes.data_as(_vp)) != 0:
+        raise ValueError("orc_batch_int_prepare failed")
+    return scale.value, var, const
