@@ -1,23 +1,32 @@
-# Top-level build: the MI355X scorer library, the C++ host-side scorer classes,
-# the C++ test drivers, and the (test-only) oracle.  No cmake; hipcc for gfx950.
+# Top-level build: the MI355X scorer library and the (test-only) oracle.  No cmake; hipcc for gfx950.
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 BUILD     = build
 LIBDIR    = rasr_amd/lib
 HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result
+# quantized kernels: MFMA results straight into VGPRs (gfx950 has one unified register file),
+# so the v_lshl_add / v_min3 epilogue reads them without v_accvgpr_read copies.
+I8FLAGS   = -mllvm -amdgpu-mfma-vgpr-form
+# float kernels: default AGPR accumulators (measured faster for the f32 MFMA chains) and one
+# tile per loop step (GMM_F32_PAIR=0), see profiles/r01/README.md
+F32FLAGS  = -DGMM_F32_PAIR=0
 HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc
-HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh
+HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh
 
 LIB       = $(LIBDIR)/librasr_gmm.so
-OBJS      = $(BUILD)/gmm_kernels.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o
+OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o
 
 all: $(LIB) oracle
 
-$(BUILD)/gmm_kernels.o: $(SRC)/gmm_kernels.hip $(HDRS)
+$(BUILD)/gmm_kernels_i8.o: $(SRC)/gmm_kernels_i8.hip $(HDRS)
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(I8FLAGS) -c $< -o $@
+
+$(BUILD)/gmm_kernels_f32.o: $(SRC)/gmm_kernels_f32.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(F32FLAGS) -c $< -o $@
 
 $(BUILD)/gmm_api.o: $(SRC)/gmm_api.cc $(HDRS)
 	@mkdir -p $(BUILD)

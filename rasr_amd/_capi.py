@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "librasr_gmm.so")
+# RASR_GMM_LIB selects another build of the same library (kernel A/B variants, scripts/ab_bench.py)
+LIB_PATH = os.environ.get("RASR_GMM_LIB") or os.path.join(_HERE, "lib", "librasr_gmm.so")
 
 GMM_OK = 0
 

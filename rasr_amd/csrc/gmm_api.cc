@@ -69,6 +69,8 @@ struct gmm_scorer {
     uint32_t          nFramesPad = 0;
     bool              multiCov   = false;
     bool              foldNorm   = false;
+    uint32_t          tileBits   = 1;
+    float             offsetK0   = 0;
     // quantized scalars
     uint32_t idxBits = 1, paddedDimension = 0;
     float    scaling = 0, scalingSquared = 0, invQ = 0, batchScale = 0;
@@ -242,6 +244,8 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.nFrameTiles = nFrameTiles;
         a.mixBase     = 0;
         a.flavor      = s->flavor == Flavor::DiagonalMaximum ? 2 : 3;
+        a.tileBits    = s->tileBits;
+        a.offsetK0    = s->offsetK0;
         a.outScale    = s->cfg.score_scale;
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
@@ -334,9 +338,11 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         s->nTiles          = p.tiling.nTiles;
         s->mixTileOff      = p.tiling.mixTileOffset;
         // one zero padding tile so the kernels may prefetch tile t+1 unconditionally
-        if ((rc = upload(reinterpret_cast<int8_t**>(&s->dTileA), p.tileA, kLanes * 16 * p.kSteps)) ||
-            (rc = upload(reinterpret_cast<int32_t**>(&s->dTileP), p.tileP, kTileRows)) ||
-            (rc = upload(&s->dTileCov, p.tiling.tileCovariance, 1)) || (rc = upload(&s->dMixTileOff, s->mixTileOff)) ||
+        // kTilePad zero tiles at the end: the kernels prefetch two tiles ahead without bound checks
+        if ((rc = upload(reinterpret_cast<int8_t**>(&s->dTileA), p.tileA, kTilePad * kLanes * 16 * p.kSteps)) ||
+            (rc = upload(reinterpret_cast<int32_t**>(&s->dTileP), p.tileP, kTilePad * kTileRows)) ||
+            (rc = upload(&s->dTileCov, p.tiling.tileCovariance, kTilePad)) ||
+            (rc = upload(&s->dMixTileOff, s->mixTileOff)) ||
             (rc = upload(&s->dIsv, p.isvDevice)))
             return rc;
         const size_t nQ = static_cast<size_t>(s->C) * s->nFramesPad;
@@ -355,11 +361,13 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         s->kSteps     = p.kSteps;
         s->multiCov   = s->C > 1;
         s->foldNorm   = p.foldNorm;
+        s->tileBits   = p.tileBits;
+        s->offsetK0   = p.offsetK0;
         s->nTiles     = p.tiling.nTiles;
         s->mixTileOff = p.tiling.mixTileOffset;
-        if ((rc = upload(reinterpret_cast<float**>(&s->dTileA), p.tileA, kLanes * p.kSteps)) ||
-            (rc = upload(&s->dTileCov, p.tiling.tileCovariance, 1)) ||
-            (rc = upload(&s->dRowDns, p.tiling.rowDensityInMixture, kTileRows)) ||
+        if ((rc = upload(reinterpret_cast<float**>(&s->dTileA), p.tileA, kTilePad * kLanes * p.kSteps)) ||
+            (rc = upload(&s->dTileCov, p.tiling.tileCovariance, kTilePad)) ||
+            (rc = upload(&s->dRowDns, p.tiling.rowDensityInMixture, kTilePad * kTileRows)) ||
             (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)))
             return rc;
         const size_t nX = static_cast<size_t>(s->C) * s->nFramesPad;

@@ -1,0 +1,59 @@
+// gmm_device.hh -- device helpers shared by the MI355X scorer kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "gmm_kernels.hh"
+
+namespace rasr_gmm {
+namespace dev {
+
+typedef int   i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef GMM_F32_PAIR
+#define GMM_F32_PAIR 1  // float kernel: two tiles per loop step
+#endif
+
+// ---------------------------------------------------------------------------
+// reference quantizer, device side (mirrors refRoundToInt / refQuantize in gmm_prepare.cc)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int refRoundToInt(float x) {
+    const float t = __fadd_rn(x, copysignf(0x1.fffffep-2f, x));
+    if (!(fabsf(t) < 2147483648.0f))
+        return INT_MIN;  // cvttss2si "integer indefinite"
+    return static_cast<int>(t);
+}
+
+// q(x) - 128 in [-128, 127]  (quantize<f32,u8>, src/Mm/Utilities.hh:186-190)
+__device__ __forceinline__ int quantizeCentered(float x) {
+    int v = static_cast<int>(static_cast<unsigned>(refRoundToInt(x)) + 128u);
+    v     = v > 255 ? 255 : v;
+    v     = v < 0 ? 0 : v;
+    return v - 128;
+}
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+
+// Workgroup -> (chunk, frame tile).  Blocks b and b+8 share an XCD (round-robin
+// dispatch); give each XCD whole chunks and walk their frame tiles back to back.
+__device__ __forceinline__ bool mapBlock(uint32_t nChunks, uint32_t nFrameTiles, uint32_t& chunk, uint32_t& ft) {
+    const uint32_t b = blockIdx.x, xcd = b & 7u, j = b >> 3;
+    chunk            = xcd + 8u * (j / nFrameTiles);
+    ft               = j % nFrameTiles;
+    return chunk < nChunks;
+}
+
+__device__ __forceinline__ void lexMin(float& v, uint32_t& i, float v2, uint32_t i2) {
+    const bool take = (v2 < v) || (v2 == v && i2 < i);
+    v               = take ? v2 : v;
+    i               = take ? i2 : i;
+}
+
+}  // namespace dev
+}  // namespace rasr_gmm

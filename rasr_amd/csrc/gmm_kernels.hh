@@ -13,6 +13,7 @@ constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kI8FramesPerBlock  = kWavesPerBlock * kI8NF * 16;   // 512
 constexpr uint32_t kF32FramesPerBlock = kWavesPerBlock * kF32NF * 16;  // 256
 constexpr uint32_t kFramePadQuantum   = 512;
+constexpr uint32_t kTilePad           = 4;    // zero tiles after the last one (two-ahead prefetch)
 
 struct I8Args {
     const void*     tileA;        // i32x4 [T+1][KS][64]
@@ -44,6 +45,8 @@ struct F32Args {
     uint32_t        nFrames, nFramesPad, scoreStride;
     uint32_t        nChunks, nFrameTiles, mixBase;
     int             flavor;       // 2 diagonal-maximum, 3 batch-float
+    uint32_t        tileBits;     // single covariance: low mantissa bits holding the tile number
+    float           offsetK0;     // single covariance: constant added to every row so values are > 0
     float           outScale;
 };
 

@@ -1,0 +1,306 @@
+// gmm_kernels.hip -- MI355X (gfx950) kernels of the diagonal-GMM feature scorer.
+//
+// Hot path: for a batch of F frames and every mixture e of the model,
+//   score(e,t) = min_{d in e} [ c_d + || A_d - x_t ||^2 ]   (+ argmin)
+// RASR computes it per frame and density with a JIT'd SSE2 u8 SSD
+// (src/Mm/SimdFeatureScorer.cc:158-176, src/Mm/SSE2CodeGenerator.cc:324-374)
+// or SSE float code (src/Mm/GaussDiagonalMaximumFeatureScorer.cc:116-218).
+// Here the cross term is a dense (densities x K) . (K x frames) contraction on
+// the matrix cores and the per-mixture minimum is a running min in the MFMA
+// accumulator registers, reduced across the wave once per mixture:
+//
+//   quantized (SIMD-diagonal-maximum, batch-int): v_mfma_i32_16x16x64_i8 on
+//     s8 operands (q - 128); exact integer arithmetic; epilogue per element is
+//     one v_lshl_add (constant + 2*dot, packed with the density index in the
+//     low bits) and one v_min_i32 -> bit-identical scores and argmins;
+//   float (diagonal-maximum, batch-float): v_mfma_f32_16x16x4_f32, the row
+//     constant folded into one K column; epilogue v_cmp + 2 v_cndmask.
+//
+// Work decomposition: one 256-thread workgroup = 4 waves x NF column blocks of
+// 16 frames; it walks a chunk of consecutive mixtures (all their tiles of 16
+// densities).  Workgroups that share a chunk are placed on one XCD (blockIdx %
+// 8) and run back to back, so each chunk's tiles are fetched from HBM/MALL into
+// that XCD's L2 once and re-read from L2 by the other frame tiles.
+//
+// Every kernel is compiled with -ffp-contract=off; the quantizer additionally
+// uses __fmul_rn / __fadd_rn so it can never be contracted into an FMA.
+//
+// This file: the quantized kernels (built with -mllvm -amdgpu-mfma-vgpr-form, see Makefile).
+#include "gmm_device.hh"
+
+namespace rasr_gmm {
+namespace dev {
+
+// ---------------------------------------------------------------------------
+// frame preparation (quantized): Context::Context, SimdFeatureScorer.cc:22-35
+//   frameQ [C][nFramesPad][KS*64] s8 (q - 128, 0 in the padding), frameSS [C][nFramesPad] = sum (q-128)^2
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prepareFramesI8(const float* __restrict__ frames, uint32_t nFrames,
+                                                        uint32_t frameStride, uint32_t nFramesPad,
+                                                        uint32_t nFramesRead, uint32_t D,
+                                                        uint32_t C, uint32_t KS, const float* __restrict__ isv,
+                                                        int8_t* __restrict__ frameQ, int32_t* __restrict__ frameSS) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= C * nFramesRead)
+        return;
+    const uint32_t c = gid / nFramesRead, f = gid % nFramesRead;
+    const float*   x  = frames + static_cast<size_t>(f) * frameStride;
+    const float*   iv = isv + static_cast<size_t>(c) * KS * 64;
+    i32x4*         out = reinterpret_cast<i32x4*>(frameQ + (static_cast<size_t>(c) * nFramesPad + f) * KS * 64);
+    int            ss = 0;
+    for (uint32_t blk = 0; blk < KS * 4; ++blk) {
+        i32x4 w;
+        for (int q4 = 0; q4 < 4; ++q4) {
+            uint32_t word = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t k = blk * 16 + q4 * 4 + b;
+                int            v = 0;
+                if (f < nFrames && k < D) {
+                    v = quantizeCentered(__fmul_rn(x[k], iv[k]));  // multiplyAndQuantize, IntelOptimization.cc:63
+                    ss += v * v;
+                }
+                word |= (static_cast<uint32_t>(v) & 0xffu) << (8 * b);
+            }
+            w[q4] = static_cast<int>(word);
+        }
+        out[blk] = w;
+    }
+    frameSS[static_cast<size_t>(c) * nFramesPad + f] = ss;
+}
+
+// ---------------------------------------------------------------------------
+// quantized scorer
+// ---------------------------------------------------------------------------
+template <int NF, int KS, bool MULTI>
+__global__ __launch_bounds__(256) void scoreI8(I8Args a) {
+    static_assert(NF == 4 || NF == 8, "NF");
+    constexpr int NPL = NF / 4;  // results per lane per mixture
+    const int     lane = threadIdx.x & 63;
+    const int     wave = threadIdx.x >> 6;
+    const int     g    = lane >> 4;
+    uint32_t      chunk, ft;
+    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
+        return;
+    const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const int      ib = static_cast<int>(a.idxBits);
+    const i32x4*   tA = static_cast<const i32x4*>(a.tileA);
+    const i32x4*   tP = static_cast<const i32x4*>(a.tileP);
+
+    // frame operands (B fragments) of covariance 0; per-lane frame = frame0 + 16 cb + (lane & 15)
+    i32x4      B[NF][KS];
+    int        ssCol[NF];  // MULTI: sum sq of the column's frame for the current covariance
+    uint32_t   curCov = 0;
+    const auto loadB  = [&](uint32_t cov) {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            const uint32_t f = frame0 + cb * 16 + (lane & 15);
+            const i32x4*   q = reinterpret_cast<const i32x4*>(
+                    a.frameQ + (static_cast<size_t>(cov) * a.nFramesPad + f) * (KS * 64)) + g;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                B[cb][ks] = q[ks * 4];
+            if constexpr (MULTI)
+                ssCol[cb] = a.frameSS[static_cast<size_t>(cov) * a.nFramesPad + f];
+        }
+    };
+    loadB(0);
+    int ssOut[NPL];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i)
+        ssOut[i] = MULTI ? 0 : a.frameSS[frame0 + 64 * i + lane];
+
+    // Tile operands in flight: (A0, P0) = tile t, (A1, P1) = tile t+1.  The tile arrays carry
+    // kTilePad zero tiles at the end, so the two-ahead prefetch never needs a bound check.
+    uint32_t   t = a.mixTileOff[m0];
+    i32x4      A0[KS], A1[KS];
+    i32x4      P0, P1;
+    const auto loadTile = [&](uint32_t tt, i32x4(&A)[KS], i32x4& P) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            A[ks] = tA[(static_cast<size_t>(tt) * KS + ks) * 64 + lane];
+        P = tP[static_cast<size_t>(tt) * 4 + g];
+    };
+    loadTile(t, A0, P0);
+    loadTile(t + 1, A1, P1);
+    const uint32_t sh = static_cast<uint32_t>(ib + 1);
+    // packed = (c + sum a'^2 + 2 dot(-a', b')) << ib | density   (see gmm_prepare.cc): one v_lshl_add
+    const auto pack = [&](int acc, int p) {
+        return static_cast<int>((static_cast<uint32_t>(acc) << sh) + static_cast<uint32_t>(p));
+    };
+
+    for (uint32_t m = m0; m < m1; ++m) {
+        const uint32_t tEnd = a.mixTileOff[m + 1];
+        int            best[NF][4];
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                best[cb][r] = INT_MAX;
+
+        if constexpr (!MULTI) {
+            // two tiles per step: 2 NF independent MFMAs, the operands of tiles t+2, t+3 loaded
+            // behind them, one v_min3 per pair of candidates
+            for (; t + 1 < tEnd; t += 2) {
+                i32x4 accA[NF], accB[NF];
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    accA[cb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks)
+                        accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
+                }
+                const i32x4 PA = P0;
+                loadTile(t + 2, A0, P0);
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    accB[cb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks)
+                        accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[ks], B[cb][ks], accB[cb], 0, 0, 0);
+                }
+                const i32x4 PB = P1;
+                loadTile(t + 3, A1, P1);
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        best[cb][r] = min(best[cb][r], min(pack(accA[cb][r], PA[r]), pack(accB[cb][r], PB[r])));
+            }
+            if (t < tEnd) {  // odd tile count: last tile alone
+                i32x4 accA[NF];
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    accA[cb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks)
+                        accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
+                }
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        best[cb][r] = min(best[cb][r], pack(accA[cb][r], P0[r]));
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    A0[ks] = A1[ks];
+                P0 = P1;
+                loadTile(t + 2, A1, P1);
+                ++t;
+            }
+        }
+        else {
+            // several covariances: the frame operand follows the tile's covariance
+            for (; t < tEnd; ++t) {
+                const uint32_t cov = a.tileCov[t];
+                if (cov != curCov) {
+                    curCov = cov;
+                    loadB(cov);
+                }
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    i32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks)
+                        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], acc, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int v = static_cast<int>(static_cast<uint32_t>(pack(acc[r], P0[r])) +
+                                                       (static_cast<uint32_t>(ssCol[cb]) << ib));
+                        best[cb][r] = min(best[cb][r], v);
+                    }
+                }
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    A0[ks] = A1[ks];
+                P0 = P1;
+                loadTile(t + 2, A1, P1);
+            }
+        }
+
+        // per-mixture reduction: 4 rows in-lane, then a reduce-scatter over the 4 lane groups
+        int v[NF];
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+            v[cb] = min(min(best[cb][0], best[cb][1]), min(best[cb][2], best[cb][3]));
+        const bool hi1 = (g >> 1) & 1, hi0 = g & 1;
+        int        w[NF / 2];  // after the xor-32 step: column blocks cb with bit1 == hi1
+#pragma unroll
+        for (int p = 0; p < NF / 2; ++p) {
+            const int c    = (p & 1) | ((p >> 1) << 2);  // 0,1,4,5: bit1 clear
+            const int send = hi1 ? v[c] : v[c ^ 2];
+            const int keep = hi1 ? v[c ^ 2] : v[c];
+            w[p]           = min(keep, __shfl_xor(send, 32));
+        }
+        int res[NPL];  // result for column block cb = g + 4 i
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int send = hi0 ? w[2 * i] : w[2 * i + 1];
+            const int keep = hi0 ? w[2 * i + 1] : w[2 * i];
+            res[i]         = min(keep, __shfl_xor(send, 16));
+        }
+
+        const uint32_t mo = m - a.mixBase;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const uint32_t f = frame0 + 64 * i + lane;
+            if (f >= a.nFrames)
+                continue;
+            const int packed = res[i];
+            int       q;
+            uint32_t  dns;
+            if (packed == INT_MAX) {  // mixture without densities: minScore stays Core::Type<int>::max
+                q   = INT_MAX;
+                dns = 0xffffffffu;
+            }
+            else {
+                q   = (packed >> ib) + ssOut[i];
+                dns = static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
+            }
+            float score;
+            if (a.flavor == 0)  // SimdFeatureScorer.cc:142: 0.5 * q / scalingSquared_ in double
+                score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
+            else  // BatchFeatureScorer.cc:468: (f32)best / scale_
+                score = __fdiv_rn(static_cast<float>(q), a.batchScale);
+            if (a.outScale != 1.0f)
+                score = __fmul_rn(a.outScale, score);  // ScaledContextScorer::score, ScaledFeatureScorer.hh:62-64
+            const size_t o = static_cast<size_t>(mo) * a.scoreStride + f;
+            a.scores[o]    = score;
+            if (a.best)
+                a.best[o] = dns;
+        }
+    }
+}
+
+}  // namespace dev
+
+using dev::prepareFramesI8;
+
+hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
+                                 uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, const float* isv,
+                                 int8_t* frameQ, int32_t* frameSS, hipStream_t stream) {
+    const uint32_t n = C * nFramesRead;
+    hipLaunchKernelGGL(prepareFramesI8, dim3((n + 255) / 256), dim3(256), 0, stream, frames, nFrames, frameStride,
+                       nFramesPad, nFramesRead, D, C, KS, isv, frameQ, frameSS);
+    return hipGetLastError();
+}
+
+template <int NF, int KS, bool MULTI>
+static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL((dev::scoreI8<NF, KS, MULTI>), dim3(grid), dim3(256), 0, s, a);
+}
+
+hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream) {
+    const uint32_t grid = 8u * ((a.nChunks + 7u) / 8u) * a.nFrameTiles;
+    if (grid == 0)
+        return hipSuccess;
+    if (kSteps == 1)
+        multiCov ? launchI8T<kI8NF, 1, true>(a, grid, stream) : launchI8T<kI8NF, 1, false>(a, grid, stream);
+    else if (kSteps == 2)
+        multiCov ? launchI8T<kI8NF, 2, true>(a, grid, stream) : launchI8T<kI8NF, 2, false>(a, grid, stream);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace rasr_gmm

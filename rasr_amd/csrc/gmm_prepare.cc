@@ -354,6 +354,39 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
 
     buildTiling(ms, shard, out.tiling);
     const uint32_t T = out.tiling.nTiles, KS = out.kSteps;
+
+    // row constant c_d (everything but the distance)
+    const auto rowConstant = [&](uint32_t e) -> double {
+        const uint32_t cov = ms.density_covariance[ms.mixture_densities[e]];
+        if (dm) {
+            // minus2LogWeights_ (MixtureFeatureScorerElement.cc:26,30-33) + logNorm (GDMFS.cc:126-129)
+            const float m2lw = static_cast<float>(-2 * ms.mixture_log_weights[e]) * mixtureWeightScale;
+            return static_cast<double>(m2lw) + static_cast<double>(out.logNorm[cov]);
+        }
+        // BatchFeatureScorer.cc:167: constants = logNormFactor - 2 * logWeight (f32)
+        return static_cast<float>(static_cast<double>(out.logNorm[cov]) - 2 * ms.mixture_log_weights[e]);
+    };
+    // Single covariance: the kernel keeps (value, tile) in one float whose low tileBits mantissa
+    // bits hold the tile number, which orders correctly only for positive values.  A row's value
+    // is ||x'-m'||^2 + c_d >= c_d, so shift every constant by K0 when some c_d < 1.
+    out.offsetK0 = 0.0f;
+    out.tileBits = 1;
+    if (!out.foldNorm) {
+        double minC = 1.0;
+        for (uint32_t e : out.tiling.rowEntry)
+            if (e != UINT32_MAX)
+                minC = std::min(minC, rowConstant(e));
+        if (minC < 1.0)
+            out.offsetK0 = static_cast<float>(std::ceil(1.0 - minC));
+        uint32_t maxTiles = 1;
+        for (uint32_t m = 0; m < out.nMixtures; ++m)
+            maxTiles = std::max(maxTiles, out.tiling.mixTileOffset[m + 1] - out.tiling.mixTileOffset[m]);
+        while ((1u << out.tileBits) < maxTiles)
+            ++out.tileBits;
+        if (out.tileBits > 8)
+            return "float scorer supports at most 4096 densities per mixture";  // key precision 2^-15
+    }
+
     out.tileA.assign(static_cast<size_t>(T) * KS * kLanes, 0.0f);
     std::vector<float> row(KS * 4);
     for (uint32_t t = 0; t < T; ++t) {
@@ -374,17 +407,7 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                     row[k]         = -2.0f * mp;
                     mm += static_cast<double>(mp) * mp;
                 }
-                double c;
-                if (dm) {
-                    // minus2LogWeights_ (MixtureFeatureScorerElement.cc:26,30-33) + logNorm (GDMFS.cc:126-129)
-                    const float m2lw = static_cast<float>(-2 * ms.mixture_log_weights[e]) * mixtureWeightScale;
-                    c = static_cast<double>(m2lw) + static_cast<double>(out.logNorm[cov]);
-                }
-                else {
-                    // BatchFeatureScorer.cc:167: constants = logNormFactor - 2 * logWeight (f32)
-                    c = static_cast<float>(static_cast<double>(out.logNorm[cov]) - 2 * ms.mixture_log_weights[e]);
-                }
-                row[D] = static_cast<float>(mm + c);
+                row[D] = static_cast<float>(mm + rowConstant(e) + out.offsetK0);
                 if (out.foldNorm)
                     row[D + 1] = 1.0f;
             }

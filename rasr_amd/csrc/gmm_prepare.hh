@@ -82,6 +82,8 @@ struct PreparedFloat {
     uint32_t dimension = 0, nCovariances = 0, nMixtures = 0;
     uint32_t kSteps = 0;              // K/4
     bool     foldNorm = false;        // multi-covariance: ||x'||^2 folded into K column dimension+1
+    uint32_t tileBits = 1;            // single covariance: ceil(log2(max tiles per mixture))
+    float    offsetK0 = 0;            // single covariance: added to every row constant (values > 0)
     std::vector<float> isv;           // [C][dimension] (after gaussian-scale)
     std::vector<float> logNorm;       // [C]
     Tiling             tiling;

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""A/B timing of library variants (scripts/build_variants.sh) on one GPU.
+
+Each variant runs in its own subprocess (RASR_GMM_LIB=<so>); rounds are interleaved
+(v1 v2 ... v1 v2 ...) and the median / min kernel time per variant is reported.
+usage: ab_bench.py --mode fp32|simd --rounds 3 lib1.so lib2.so ...
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import os, sys, json, time
+sys.path.insert(0, os.environ["ROOT"])
+import torch, rasr_amd as ra
+mode = os.environ["MODE"]; F = int(os.environ["FRAMES"])
+kind = "diagonal-maximum" if mode == "fp32" else "SIMD-diagonal-maximum"
+ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
+sc = ra.Scorer(ms, kind, max_frames=F)
+fr = torch.from_numpy(ra.synthetic_frames(F, 39, seed=5)).cuda()
+out = torch.empty((5000, F), dtype=torch.float32, device="cuda")
+best = torch.empty((5000, F), dtype=torch.int32, device="cuda")
+for _ in range(3): sc.score_device(fr, out, best)
+torch.cuda.synchronize(); sc.set_timing(True)
+for _ in range(int(os.environ["STEPS"])): sc.score_device(fr, out, best)
+ms_, n = sc.kernel_time()
+print(json.dumps({"kernel_ms": ms_ / n, "checksum": float(out[:, :64].double().sum())}))
+'''
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="fp32")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--frames", type=int, default=0)
+    ap.add_argument("libs", nargs="+")
+    a = ap.parse_args()
+    frames = a.frames or (8192 if a.mode == "fp32" else 32768)
+    res = {lib: [] for lib in a.libs}
+    sums = {}
+    for _ in range(a.rounds):
+        for lib in a.libs:
+            env = dict(os.environ, RASR_GMM_LIB=os.path.abspath(lib), ROOT=ROOT, MODE=a.mode, FRAMES=str(frames),
+                       STEPS=str(a.steps))
+            p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+            if p.returncode != 0:
+                print(lib, "FAILED", p.stderr[-2000:])
+                sys.exit(p.returncode)
+            r = json.loads(p.stdout.strip().splitlines()[-1])
+            res[lib].append(r["kernel_ms"])
+            sums[lib] = r["checksum"]
+    for lib, v in res.items():
+        fps = frames / (statistics.median(v) * 1e-3)
+        print(f"{os.path.basename(lib):40s} median {statistics.median(v):.4f} ms  min {min(v):.4f}  "
+              f"{fps / 1e6:.3f} Mframes/s  checksum {sums[lib]:.6f}")
+
+
+if __name__ == "__main__":
+    main()
