@@ -14,6 +14,12 @@ namespace dev {
 typedef int   i32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef GMM_PERMLANE
+#define GMM_PERMLANE 1  // quantized kernel: reduce-scatter by v_permlane{32,16}_swap (else ds_bpermute)
+#endif
+#ifndef GMM_I8_LDS
+#define GMM_I8_LDS 1  // quantized kernel, one covariance: tiles staged through LDS (scoreI8Seg)
+#endif
 #ifndef GMM_F32_PAIR
 #define GMM_F32_PAIR 1  // float kernel: two tiles per loop step
 #endif
@@ -53,6 +59,34 @@ __device__ __forceinline__ void lexMin(float& v, uint32_t& i, float v2, uint32_t
     const bool take = (v2 < v) || (v2 == v && i2 < i);
     v               = take ? v2 : v;
     i               = take ? i2 : i;
+}
+
+// Cross-lane exchanges of the per-mixture reduce-scatter, as VALU permutes (no LDS round trip).
+// v_permlane32_swap(x, y) swaps x's lanes 32..63 with y's lanes 0..31; v_permlane16_swap(x, y)
+// swaps x's odd 16-lane rows with y's even rows.  Taking min(x', y') afterwards leaves, in every
+// lane, the minimum over the lane and its partner (lane ^ 32, resp. lane ^ 16) of x in the lanes
+// that keep x and of y in the lanes that keep y: one swap + one min per exchanged pair.
+__device__ __forceinline__ int swapMin32(int x, int y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    return min(static_cast<int>(r[0]), static_cast<int>(r[1]));
+}
+__device__ __forceinline__ int swapMin16(int x, int y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    return min(static_cast<int>(r[0]), static_cast<int>(r[1]));
+}
+__device__ __forceinline__ void swapLexMin32(float xv, uint32_t xi, float yv, uint32_t yi, float& v, uint32_t& i) {
+    const auto rv = __builtin_amdgcn_permlane32_swap(__float_as_uint(xv), __float_as_uint(yv), false, false);
+    const auto ri = __builtin_amdgcn_permlane32_swap(xi, yi, false, false);
+    v             = __uint_as_float(rv[0]);
+    i             = ri[0];
+    lexMin(v, i, __uint_as_float(rv[1]), ri[1]);
+}
+__device__ __forceinline__ void swapLexMin16(float xv, uint32_t xi, float yv, uint32_t yi, float& v, uint32_t& i) {
+    const auto rv = __builtin_amdgcn_permlane16_swap(__float_as_uint(xv), __float_as_uint(yv), false, false);
+    const auto ri = __builtin_amdgcn_permlane16_swap(xi, yi, false, false);
+    v             = __uint_as_float(rv[0]);
+    i             = ri[0];
+    lexMin(v, i, __uint_as_float(rv[1]), ri[1]);
 }
 
 }  // namespace dev

@@ -7,13 +7,19 @@
 
 namespace rasr_gmm {
 
-constexpr int      kI8NF          = 8;   // column blocks of 16 frames per wave, quantized kernel
-constexpr int      kF32NF         = 4;   // column blocks of 16 frames per wave, float kernel
+#ifndef GMM_I8_NF
+#define GMM_I8_NF 8
+#endif
+#ifndef GMM_F32_NF
+#define GMM_F32_NF 4
+#endif
+constexpr int      kI8NF          = GMM_I8_NF;   // column blocks of 16 frames per wave, quantized kernel
+constexpr int      kF32NF         = GMM_F32_NF;  // column blocks of 16 frames per wave, float kernel
 constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kI8FramesPerBlock  = kWavesPerBlock * kI8NF * 16;   // 512
 constexpr uint32_t kF32FramesPerBlock = kWavesPerBlock * kF32NF * 16;  // 256
 constexpr uint32_t kFramePadQuantum   = 512;
-constexpr uint32_t kTilePad           = 4;    // zero tiles after the last one (two-ahead prefetch)
+constexpr uint32_t kTilePad           = 16;   // zero tiles after the last one (prefetch / LDS segments)
 
 struct I8Args {
     const void*     tileA;        // i32x4 [T+1][KS][64]

@@ -227,28 +227,19 @@ __global__ __launch_bounds__(256) void scoreF32(F32Args a) {
                 lexMin(v[cb], vi[cb], val, dns);
             }
         }
-        const bool hi1 = (g >> 1) & 1, hi0 = g & 1;
-        float      w[NF / 2];
-        uint32_t   wi[NF / 2];
+        float    w[NF / 2];
+        uint32_t wi[NF / 2];
 #pragma unroll
         for (int p = 0; p < NF / 2; ++p) {
-            const int      c  = (p & 1) | ((p >> 1) << 2);
-            const float    sv = hi1 ? v[c] : v[c ^ 2];
-            const uint32_t si = hi1 ? vi[c] : vi[c ^ 2];
-            float          kv = hi1 ? v[c ^ 2] : v[c];
-            uint32_t       ki = hi1 ? vi[c ^ 2] : vi[c];
-            lexMin(kv, ki, __shfl_xor(sv, 32), static_cast<uint32_t>(__shfl_xor(static_cast<int>(si), 32)));
-            w[p]  = kv;
-            wi[p] = ki;
+            const int c = (p & 1) | ((p >> 1) << 2);
+            swapLexMin32(v[c], vi[c], v[c ^ 2], vi[c ^ 2], w[p], wi[p]);
         }
         const uint32_t mo = m - a.mixBase;
 #pragma unroll
         for (int i = 0; i < NPL; ++i) {
-            const float    sv = hi0 ? w[2 * i] : w[2 * i + 1];
-            const uint32_t si = hi0 ? wi[2 * i] : wi[2 * i + 1];
-            float          kv = hi0 ? w[2 * i + 1] : w[2 * i];
-            uint32_t       ki = hi0 ? wi[2 * i + 1] : wi[2 * i];
-            lexMin(kv, ki, __shfl_xor(sv, 16), static_cast<uint32_t>(__shfl_xor(static_cast<int>(si), 16)));
+            float    kv;
+            uint32_t ki;
+            swapLexMin16(w[2 * i], wi[2 * i], w[2 * i + 1], wi[2 * i + 1], kv, ki);
             const uint32_t f = frame0 + 64 * i + lane;
             if (f >= a.nFrames)
                 continue;

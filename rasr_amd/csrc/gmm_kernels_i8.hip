@@ -71,6 +71,77 @@ __global__ __launch_bounds__(256) void prepareFramesI8(const float* __restrict__
 // ---------------------------------------------------------------------------
 // quantized scorer
 // ---------------------------------------------------------------------------
+// Per-mixture end: 4 rows in-lane, reduce-scatter over the 4 lane groups, finalize and store the
+// scores (and best densities) of the wave's NF*16 frames for mixture m.
+template <int NF>
+__device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict__ scores, uint32_t* __restrict__ bestOut,
+                                              const int (&best)[NF][4], uint32_t m, uint32_t frame0, int lane, int g,
+                                              int ib, const int (&ssOut)[NF / 4]) {
+    constexpr int NPL = NF / 4;
+    // per-mixture reduction: 4 rows in-lane, then a reduce-scatter over the 4 lane groups
+    int v[NF];
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb)
+        v[cb] = min(min(best[cb][0], best[cb][1]), min(best[cb][2], best[cb][3]));
+    int w[NF / 2];  // after the lane^32 step: column blocks cb with bit1 == (g >> 1)
+    int res[NPL];   // after the lane^16 step: column block cb = g + 4 i
+#if GMM_PERMLANE
+#pragma unroll
+    for (int p = 0; p < NF / 2; ++p) {
+        const int c = (p & 1) | ((p >> 1) << 2);  // 0,1,4,5: bit1 clear
+        w[p]        = swapMin32(v[c], v[c ^ 2]);
+    }
+#pragma unroll
+    for (int i = 0; i < NPL; ++i)
+        res[i] = swapMin16(w[2 * i], w[2 * i + 1]);
+#else
+    const bool hi1 = (g >> 1) & 1, hi0 = g & 1;
+#pragma unroll
+    for (int p = 0; p < NF / 2; ++p) {
+        const int c    = (p & 1) | ((p >> 1) << 2);
+        const int send = hi1 ? v[c] : v[c ^ 2];
+        const int keep = hi1 ? v[c ^ 2] : v[c];
+        w[p]           = min(keep, __shfl_xor(send, 32));
+    }
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int send = hi0 ? w[2 * i] : w[2 * i + 1];
+        const int keep = hi0 ? w[2 * i + 1] : w[2 * i];
+        res[i]         = min(keep, __shfl_xor(send, 16));
+    }
+#endif
+
+    const uint32_t mo = m;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const uint32_t f = frame0 + 64 * i + lane;
+        if (f >= a.nFrames)
+            continue;
+        const int packed = res[i];
+        int       q;
+        uint32_t  dns;
+        if (packed == INT_MAX) {  // mixture without densities: minScore stays Core::Type<int>::max
+            q   = INT_MAX;
+            dns = 0xffffffffu;
+        }
+        else {
+            q   = (packed >> ib) + ssOut[i];
+            dns = static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
+        }
+        float score;
+        if (a.flavor == 0)  // SimdFeatureScorer.cc:142: 0.5 * q / scalingSquared_ in double
+            score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
+        else  // BatchFeatureScorer.cc:468: (f32)best / scale_
+            score = __fdiv_rn(static_cast<float>(q), a.batchScale);
+        if (a.outScale != 1.0f)
+            score = __fmul_rn(a.outScale, score);  // ScaledContextScorer::score, ScaledFeatureScorer.hh:62-64
+        const size_t o = static_cast<size_t>(mo) * a.scoreStride + f;
+        scores[o]      = score;
+        if (bestOut)
+            bestOut[o] = dns;
+    }
+}
+
 template <int NF, int KS, bool MULTI>
 __global__ __launch_bounds__(256) void scoreI8(I8Args a) {
     static_assert(NF == 4 || NF == 8, "NF");
@@ -218,57 +289,183 @@ __global__ __launch_bounds__(256) void scoreI8(I8Args a) {
             }
         }
 
-        // per-mixture reduction: 4 rows in-lane, then a reduce-scatter over the 4 lane groups
-        int v[NF];
+        emitMixtureI8<NF>(a, a.scores, a.best, best, m, frame0, lane, g, ib, ssOut);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// quantized scorer, single covariance, tile operands staged through LDS
+//
+// The four waves of a workgroup read the same tiles (they differ only in
+// frames), so the tiles are fetched once per workgroup into an LDS ring of two
+// segments of kSegTiles tiles by LDS-DMA (global_load_lds_dwordx4: one 1 KiB
+// wave-instruction per 1 KiB operand block), a whole segment ahead of use.
+// Per segment: wait for its DMA (counted vmcnt: every wave issues the same
+// number of pieces), barrier, compute from LDS, barrier, refill the buffer with
+// the segment after next.  Mixture boundaries are independent of segment
+// boundaries.
+// ---------------------------------------------------------------------------
+constexpr int kSegTiles = 8;
+
+// mixTileOff / scores / best are separate __restrict__ parameters so the mixture boundaries are read
+// with scalar loads (a vector load would need an s_waitcnt vmcnt(0) that drains the LDS-DMA queue).
+template <int NF, int KS>
+__global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
+                                                   float* __restrict__ scores, uint32_t* __restrict__ bestOut) {
+    static_assert(NF == 4 || NF == 8, "NF");
+    constexpr int      NPL       = NF / 4;
+    constexpr uint32_t kTileA    = KS * 1024;                   // operand bytes per tile
+    constexpr uint32_t kSegA     = kSegTiles * kTileA;
+    constexpr uint32_t kSegBytes = kSegA + kSegTiles * 64;      // + packed row constants
+    constexpr int      kPieces   = kSegTiles * KS / 4;          // 1 KiB pieces per wave per segment
+    static_assert(kSegTiles * KS % 4 == 0, "segment pieces must split evenly over 4 waves");
+    // one __shared__ array only (a second one can make hipcc drain vmcnt before LDS reads)
+    __shared__ __attribute__((aligned(16))) int8_t lds[2 * kSegBytes];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int g    = lane >> 4;
+    uint32_t  chunk, ft;
+    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
+        return;  // uniform over the workgroup, before any barrier
+    const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const int      ib = static_cast<int>(a.idxBits);
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
+    const uint32_t nSeg = (T1 - T0 + kSegTiles - 1) / kSegTiles;
+    const int8_t*  gA   = static_cast<const int8_t*>(a.tileA);
+    const int8_t*  gP   = static_cast<const int8_t*>(a.tileP);
+
+    // issue segment s into buffer (s & 1); tile arrays are padded by kTilePad >= kSegTiles tiles
+    const auto issueSeg = [&](uint32_t s) {
+        const uint32_t t0   = T0 + s * kSegTiles;
+        int8_t*        base = lds + (s & 1u) * kSegBytes;
+#pragma unroll
+        for (int i = 0; i < kPieces; ++i) {
+            const uint32_t piece = static_cast<uint32_t>(wave * kPieces + i);
+            __builtin_amdgcn_global_load_lds(gA + static_cast<size_t>(t0) * kTileA + piece * 1024u + lane * 16,
+                                             base + piece * 1024u, 16, 0, 0);
+        }
+        if (lane < 8)  // 8 tiles x 64 B of row constants: 128 B per wave
+            __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * 128 + lane * 16,
+                                             base + kSegA + wave * 128, 16, 0, 0);
+    };
+    if (nSeg > 0)
+        issueSeg(0);
+    if (nSeg > 1)
+        issueSeg(1);
+
+    i32x4 B[NF][KS];
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb) {
+        const uint32_t f = frame0 + cb * 16 + (lane & 15);
+        const i32x4*   q = reinterpret_cast<const i32x4*>(a.frameQ + static_cast<size_t>(f) * (KS * 64)) + g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            B[cb][ks] = q[ks * 4];
+    }
+    int ssOut[NPL];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i)
+        ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
+
+    const uint32_t sh   = static_cast<uint32_t>(ib + 1);
+    const auto     pack = [&](int acc, int p) {
+        return static_cast<int>((static_cast<uint32_t>(acc) << sh) + static_cast<uint32_t>(p));
+    };
+    int best[NF][4];
+    const auto resetBest = [&]() {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
-            v[cb] = min(min(best[cb][0], best[cb][1]), min(best[cb][2], best[cb][3]));
-        const bool hi1 = (g >> 1) & 1, hi0 = g & 1;
-        int        w[NF / 2];  // after the xor-32 step: column blocks cb with bit1 == hi1
 #pragma unroll
-        for (int p = 0; p < NF / 2; ++p) {
-            const int c    = (p & 1) | ((p >> 1) << 2);  // 0,1,4,5: bit1 clear
-            const int send = hi1 ? v[c] : v[c ^ 2];
-            const int keep = hi1 ? v[c ^ 2] : v[c];
-            w[p]           = min(keep, __shfl_xor(send, 32));
-        }
-        int res[NPL];  // result for column block cb = g + 4 i
-#pragma unroll
-        for (int i = 0; i < NPL; ++i) {
-            const int send = hi0 ? w[2 * i] : w[2 * i + 1];
-            const int keep = hi0 ? w[2 * i + 1] : w[2 * i];
-            res[i]         = min(keep, __shfl_xor(send, 16));
-        }
+            for (int r = 0; r < 4; ++r)
+                best[cb][r] = INT_MAX;
+    };
+    resetBest();
+    uint32_t m    = m0;
+    uint32_t tEnd = mixTileOff[m0 + 1];
+    // mixtures without tiles at the start of the chunk
+    while (m < m1 && tEnd == T0) {
+        emitMixtureI8<NF>(a, scores, bestOut, best, m, frame0, lane, g, ib, ssOut);
+        ++m;
+        tEnd = m < m1 ? mixTileOff[m + 1] : T1;
+    }
 
-        const uint32_t mo = m - a.mixBase;
+    for (uint32_t s = 0; s < nSeg; ++s) {
+        // this segment's pieces (issued one segment ago) have landed; the next segment's stay in flight
+        if (s + 1 < nSeg)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPieces + 1) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const int8_t*  base   = lds + (s & 1u) * kSegBytes;
+        const uint32_t segT0  = T0 + s * kSegTiles;
+        const uint32_t segEnd = min(segT0 + kSegTiles, T1);
+        uint32_t       t      = segT0;
+        while (t < segEnd) {
+            const uint32_t lt = t - segT0;
+            if (t + 1 < segEnd && t + 1 < tEnd) {
+                // two tiles of the same mixture: 2 NF independent MFMAs, one v_min3 per candidate pair
+                i32x4 A0[KS], A1[KS];
 #pragma unroll
-        for (int i = 0; i < NPL; ++i) {
-            const uint32_t f = frame0 + 64 * i + lane;
-            if (f >= a.nFrames)
-                continue;
-            const int packed = res[i];
-            int       q;
-            uint32_t  dns;
-            if (packed == INT_MAX) {  // mixture without densities: minScore stays Core::Type<int>::max
-                q   = INT_MAX;
-                dns = 0xffffffffu;
+                for (int ks = 0; ks < KS; ++ks) {
+                    A0[ks] = *reinterpret_cast<const i32x4*>(base + lt * kTileA + ks * 1024 + lane * 16);
+                    A1[ks] = *reinterpret_cast<const i32x4*>(base + (lt + 1) * kTileA + ks * 1024 + lane * 16);
+                }
+                const i32x4 P0 = *reinterpret_cast<const i32x4*>(base + kSegA + lt * 64 + g * 16);
+                const i32x4 P1 = *reinterpret_cast<const i32x4*>(base + kSegA + (lt + 1) * 64 + g * 16);
+                i32x4       accA[NF], accB[NF];
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    accA[cb] = i32x4{0, 0, 0, 0};
+                    accB[cb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks) {
+                        accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
+                        accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[ks], B[cb][ks], accB[cb], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        best[cb][r] = min(best[cb][r], min(pack(accA[cb][r], P0[r]), pack(accB[cb][r], P1[r])));
+                t += 2;
             }
             else {
-                q   = (packed >> ib) + ssOut[i];
-                dns = static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
+                i32x4 A0[KS];
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    A0[ks] = *reinterpret_cast<const i32x4*>(base + lt * kTileA + ks * 1024 + lane * 16);
+                const i32x4 P0 = *reinterpret_cast<const i32x4*>(base + kSegA + lt * 64 + g * 16);
+                i32x4       accA[NF];
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    accA[cb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks)
+                        accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
+                }
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        best[cb][r] = min(best[cb][r], pack(accA[cb][r], P0[r]));
+                t += 1;
             }
-            float score;
-            if (a.flavor == 0)  // SimdFeatureScorer.cc:142: 0.5 * q / scalingSquared_ in double
-                score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
-            else  // BatchFeatureScorer.cc:468: (f32)best / scale_
-                score = __fdiv_rn(static_cast<float>(q), a.batchScale);
-            if (a.outScale != 1.0f)
-                score = __fmul_rn(a.outScale, score);  // ScaledContextScorer::score, ScaledFeatureScorer.hh:62-64
-            const size_t o = static_cast<size_t>(mo) * a.scoreStride + f;
-            a.scores[o]    = score;
-            if (a.best)
-                a.best[o] = dns;
+            // mixture(s) ending here (further ones without tiles end at the same point)
+            while (t == tEnd && m < m1) {
+                emitMixtureI8<NF>(a, scores, bestOut, best, m, frame0, lane, g, ib, ssOut);
+                resetBest();
+                ++m;
+                tEnd = m < m1 ? mixTileOff[m + 1] : T1;
+            }
         }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (s & 1)
+        if (s + 2 < nSeg)
+            issueSeg(s + 2);
     }
 }
 
@@ -287,6 +484,12 @@ hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t
 
 template <int NF, int KS, bool MULTI>
 static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
+#if GMM_I8_LDS
+    if constexpr (!MULTI) {
+        hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff, a.scores, a.best);
+        return;
+    }
+#endif
     hipLaunchKernelGGL((dev::scoreI8<NF, KS, MULTI>), dim3(grid), dim3(256), 0, s, a);
 }
 
