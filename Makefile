@@ -1,4 +1,5 @@
-# Top-level build: the MI355X scorer library and the (test-only) oracle.  No cmake; hipcc for gfx950.
+# Top-level build: the MI355X scorer library (HIP kernels + C-ABI + C++ host-side scorer
+# classes), the C++ protocol test driver, and the (test-only) oracle.  No cmake; hipcc for gfx950.
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 BUILD     = build
@@ -8,17 +9,20 @@ HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 # so the v_lshl_add / v_min3 epilogue reads them without v_accvgpr_read copies.
 I8FLAGS   = -mllvm -amdgpu-mfma-vgpr-form
 # float kernels: default AGPR accumulators (measured faster for the f32 MFMA chains) and one
-# tile per loop step (GMM_F32_PAIR=0), see profiles/r01/README.md
+# tile per loop step (GMM_F32_PAIR=0), see DESIGN.md "Measurements"
 F32FLAGS  = -DGMM_F32_PAIR=0
 HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc
-HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh
+HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh \
+            $(SRC)/host/GpuFeatureScorer.hh
 
 LIB       = $(LIBDIR)/librasr_gmm.so
-OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o
+OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
+            $(BUILD)/GpuFeatureScorer.o
+DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
-all: $(LIB) oracle
+all: $(LIB) $(DRIVER) oracle
 
 $(BUILD)/gmm_kernels_i8.o: $(SRC)/gmm_kernels_i8.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -36,9 +40,17 @@ $(BUILD)/gmm_prepare.o: $(SRC)/gmm_prepare.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
+$(BUILD)/GpuFeatureScorer.o: $(SRC)/host/GpuFeatureScorer.cc $(HDRS)
+	@mkdir -p $(BUILD)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+$(DRIVER): tests/cpp/feature_scorer_driver.cc $(LIB) $(HDRS)
+	@mkdir -p $(BUILD)/tests
+	g++ $(HOSTFLAGS) -o $@ $< -L$(LIBDIR) -lrasr_gmm -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 oracle:
 	$(MAKE) -C oracle

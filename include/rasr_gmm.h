@@ -86,6 +86,7 @@ int gmm_scorer_destroy(gmm_scorer* scorer);
 /* FeatureScorer::nMixtures() (FeatureScorer.hh:49), AssigningFeatureScorer::dimension(). */
 uint32_t gmm_scorer_n_mixtures(const gmm_scorer* scorer);
 uint32_t gmm_scorer_dimension(const gmm_scorer* scorer);
+uint32_t gmm_scorer_n_covariances(const gmm_scorer* scorer);  /* MixtureSet::nCovariances() */
 int      gmm_scorer_type_of(const gmm_scorer* scorer);
 
 /* Score n_frames feature vectors (row t at frames + t * frame_stride floats)

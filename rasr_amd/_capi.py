@@ -73,6 +73,7 @@ PROTOTYPES = [
     ("gmm_scorer_destroy", ctypes.c_int, [ctypes.c_void_p]),
     ("gmm_scorer_n_mixtures", ctypes.c_uint32, [ctypes.c_void_p]),
     ("gmm_scorer_dimension", ctypes.c_uint32, [ctypes.c_void_p]),
+    ("gmm_scorer_n_covariances", ctypes.c_uint32, [ctypes.c_void_p]),
     ("gmm_scorer_type_of", ctypes.c_int, [ctypes.c_void_p]),
     ("gmm_score_device", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,

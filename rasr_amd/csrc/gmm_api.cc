@@ -398,6 +398,10 @@ uint32_t gmm_scorer_dimension(const gmm_scorer* s) {
     return s ? s->D : 0;
 }
 
+uint32_t gmm_scorer_n_covariances(const gmm_scorer* s) {
+    return s ? s->C : 0;
+}
+
 int gmm_scorer_type_of(const gmm_scorer* s) {
     return s ? static_cast<int>(s->type) : -1;
 }

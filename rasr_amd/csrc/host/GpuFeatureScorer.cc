@@ -1,0 +1,320 @@
+// GpuFeatureScorer.cc -- see GpuFeatureScorer.hh.
+#include "GpuFeatureScorer.hh"
+
+#include <cassert>
+#include <cstring>
+
+namespace Mm {
+namespace Gpu {
+
+// ---------------------------------------------------------------------------
+// MixtureSet
+// ---------------------------------------------------------------------------
+uint32_t MixtureSet::addMean(const std::vector<float>& mean) {
+    assert(mean.size() == dimension_);
+    means_.insert(means_.end(), mean.begin(), mean.end());
+    return static_cast<uint32_t>(means_.size() / dimension_ - 1);
+}
+
+uint32_t MixtureSet::addCovariance(const std::vector<float>& diagonal) {
+    assert(diagonal.size() == dimension_);
+    variances_.insert(variances_.end(), diagonal.begin(), diagonal.end());
+    return static_cast<uint32_t>(variances_.size() / dimension_ - 1);
+}
+
+uint32_t MixtureSet::addDensity(uint32_t meanIndex, uint32_t covarianceIndex) {
+    densityMean_.push_back(meanIndex);
+    densityCovariance_.push_back(covarianceIndex);
+    return static_cast<uint32_t>(densityMean_.size() - 1);
+}
+
+uint32_t MixtureSet::addMixture(const std::vector<uint32_t>& densities, const std::vector<double>& logWeights) {
+    assert(densities.size() == logWeights.size());
+    mixtureDensities_.insert(mixtureDensities_.end(), densities.begin(), densities.end());
+    mixtureLogWeights_.insert(mixtureLogWeights_.end(), logWeights.begin(), logWeights.end());
+    mixtureOffsets_.push_back(static_cast<uint32_t>(mixtureDensities_.size()));
+    return nMixtures() - 1;
+}
+
+gmm_mixture_set MixtureSet::descriptor() const {
+    gmm_mixture_set d;
+    std::memset(&d, 0, sizeof(d));
+    d.dimension           = dimension_;
+    d.n_means             = dimension_ ? static_cast<uint32_t>(means_.size() / dimension_) : 0;
+    d.means               = means_.data();
+    d.n_covariances       = dimension_ ? static_cast<uint32_t>(variances_.size() / dimension_) : 0;
+    d.variances           = variances_.data();
+    d.n_densities         = nDensities();
+    d.density_mean        = densityMean_.data();
+    d.density_covariance  = densityCovariance_.data();
+    d.n_mixtures          = nMixtures();
+    d.mixture_offsets     = mixtureOffsets_.data();
+    d.mixture_densities   = mixtureDensities_.data();
+    d.mixture_log_weights = mixtureLogWeights_.data();
+    return d;
+}
+
+// ---------------------------------------------------------------------------
+// FeatureScorer
+// ---------------------------------------------------------------------------
+static bool typeOf(const std::string& name, gmm_scorer_type* t, bool* assigning, bool* batch) {
+    struct {
+        const char*     name;
+        gmm_scorer_type type;
+        bool            assigning, batch;
+    } const table[] = {
+            {"SIMD-diagonal-maximum", GMM_SIMD_DIAGONAL_MAXIMUM, true, false},
+            {"diagonal-maximum", GMM_DIAGONAL_MAXIMUM, true, false},
+            {"batch-diagonal-maximum-int", GMM_BATCH_DIAGONAL_MAXIMUM_INT, false, true},
+            {"batch-diagonal-maximum-fast", GMM_BATCH_DIAGONAL_MAXIMUM_FAST, false, true},
+            {"batch-diagonal-maximum-float", GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT, false, true},
+    };
+    for (const auto& e : table)
+        if (name == e.name) {
+            *t         = e.type;
+            *assigning = e.assigning;
+            *batch     = e.batch;
+            return true;
+        }
+    return false;
+}
+
+FeatureScorer::~FeatureScorer() {
+    gmm_scorer_destroy(handle_);
+}
+
+bool FeatureScorer::init(const MixtureSet& ms, const Configuration& c, uint32_t maxFrames, std::string* error) {
+    gmm_scorer_type t;
+    bool            batch = false;
+    if (!typeOf(c.type, &t, &assigning_, &batch)) {
+        if (error)
+            *error = "unknown feature scorer type: " + c.type;
+        return false;
+    }
+    config_ = c;
+    gmm_scorer_config cfg;
+    gmm_default_config(&cfg);
+    cfg.mixture_weight_scale = c.mixtureWeightScale;
+    cfg.gaussian_scale       = c.gaussianScale;
+    cfg.score_scale          = c.scale;
+    cfg.max_frames           = maxFrames;
+    const gmm_mixture_set d  = ms.descriptor();
+    if (gmm_scorer_create(&d, t, &cfg, c.device, &handle_) != GMM_OK) {
+        if (error)
+            *error = gmm_last_error();
+        handle_ = nullptr;
+        return false;
+    }
+    nMixtures_ = gmm_scorer_n_mixtures(handle_);
+    dimension_ = gmm_scorer_dimension(handle_);
+    return true;
+}
+
+float FeatureScorer::inverseQuantizationFactor() const {
+    float s = 0, q = 0;
+    gmm_scorer_quantization(handle_, &s, &q);
+    return q;
+}
+
+std::vector<std::vector<uint8_t>> FeatureScorer::multiplyAndQuantize(const FeatureVector& f) const {
+    assert(f.size() == dimension_);
+    const uint32_t                    dp = (dimension_ + 15) / 16 * 16;
+    const uint32_t                    nc = gmm_scorer_n_covariances(handle_);
+    std::vector<uint8_t>              buf(static_cast<size_t>(dp) * nc);
+    std::vector<std::vector<uint8_t>> out;
+    if (gmm_scorer_multiply_and_quantize(handle_, f.data(), buf.data()) != GMM_OK)
+        return out;
+    for (uint32_t c = 0; c < nc; ++c)
+        out.emplace_back(buf.begin() + static_cast<size_t>(c) * dp, buf.begin() + static_cast<size_t>(c + 1) * dp);
+    return out;
+}
+
+// ---------------------------------------------------------------------------
+// ContextScorers
+// ---------------------------------------------------------------------------
+namespace {
+
+// one frame, all mixtures, owned scores (SimdGaussDiagonalMaximumFeatureScorer::Context)
+class FrameScorer : public ContextScorer {
+public:
+    FrameScorer(std::vector<float>&& s, std::vector<uint32_t>&& b, bool assigning)
+            : scores_(std::move(s)), best_(std::move(b)), assigning_(assigning) {}
+    EmissionIndex nEmissions() const override { return static_cast<EmissionIndex>(scores_.size()); }
+    Score         score(EmissionIndex e) const override {
+        assert(e < scores_.size());
+        return scores_[e];
+    }
+    bool             hasBestDensity() const override { return assigning_; }
+    DensityInMixture bestDensity(EmissionIndex e) const override {
+        assert(e < best_.size());
+        return best_[e];
+    }
+
+private:
+    std::vector<float>    scores_;
+    std::vector<uint32_t> best_;
+    bool                  assigning_;
+};
+
+// BatchFeatureScorerBase::ContextScorer (BatchFeatureScorer.hh:42-60)
+class BufferedScorer : public ContextScorer {
+public:
+    BufferedScorer(const GpuBatchFeatureScorer* parent, uint32_t currentFeature, uint32_t buffered, bool assigning)
+            : parent_(parent), currentFeature_(currentFeature), buffered_(buffered), assigning_(assigning) {}
+    EmissionIndex nEmissions() const override { return parent_->nMixtures(); }
+    Score         score(EmissionIndex e) const override { return parent_->getScore(e, currentFeature_, buffered_); }
+    bool             hasBestDensity() const override { return assigning_; }
+    DensityInMixture bestDensity(EmissionIndex e) const override {
+        return parent_->getBestDensity(e, currentFeature_, buffered_);
+    }
+
+private:
+    const GpuBatchFeatureScorer* parent_;
+    uint32_t                     currentFeature_, buffered_;
+    bool                         assigning_;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// GpuFeatureScorer
+// ---------------------------------------------------------------------------
+std::unique_ptr<GpuFeatureScorer> GpuFeatureScorer::create(const MixtureSet& ms, const Configuration& c,
+                                                           std::string* error) {
+    std::unique_ptr<GpuFeatureScorer> s(new GpuFeatureScorer());
+    if (!s->init(ms, c, 1, error))
+        return nullptr;
+    return s;
+}
+
+Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
+    assert(f.size() == dimension_);  // require(featureVector.size() == dimension()), SimdFeatureScorer.cc:26
+    std::vector<float>    s(nMixtures_);
+    std::vector<uint32_t> b(nMixtures_);
+    if (gmm_score_host(handle_, f.data(), 1, dimension_, s.data(), assigning_ ? b.data() : nullptr, 1) != GMM_OK)
+        return Scorer();
+    return std::make_shared<FrameScorer>(std::move(s), std::move(b), assigning_);
+}
+
+// ---------------------------------------------------------------------------
+// GpuBatchFeatureScorer
+// ---------------------------------------------------------------------------
+std::unique_ptr<GpuBatchFeatureScorer> GpuBatchFeatureScorer::create(const MixtureSet& ms, const Configuration& c,
+                                                                     std::string* error) {
+    std::unique_ptr<GpuBatchFeatureScorer> s(new GpuBatchFeatureScorer());
+    const uint32_t                         b = c.bufferSize ? c.bufferSize : 1;
+    if (!s->init(ms, c, b, error))
+        return nullptr;
+    s->bufferSize_ = b;
+    s->features_.assign(static_cast<size_t>(b) * s->dimension_, 0.0f);
+    s->scores_.assign(static_cast<size_t>(s->nMixtures_) * b, 0.0f);
+    s->best_.assign(static_cast<size_t>(s->nMixtures_) * b, 0xffffffffu);
+    s->cached_.assign(b, 0);
+    s->gather_.resize(static_cast<size_t>(b) * s->dimension_);
+    s->gatherScores_.resize(static_cast<size_t>(s->nMixtures_) * b);
+    s->gatherBest_.resize(static_cast<size_t>(s->nMixtures_) * b);
+    return s;
+}
+
+// BatchFeatureScorerBase::reset, BatchFeatureScorer.cc:40-44
+void GpuBatchFeatureScorer::reset() const {
+    std::fill(cached_.begin(), cached_.end(), 0);
+    currentFeature_ = 0;
+    buffered_       = 0;
+}
+
+void GpuBatchFeatureScorer::setFeature(size_t pos, const FeatureVector& f) const {
+    assert(pos < bufferSize_ && f.size() == dimension_);
+    std::copy(f.begin(), f.end(), features_.begin() + pos * dimension_);
+}
+
+// BatchFeatureScorerBase::addFeature, BatchFeatureScorer.cc:46-50
+void GpuBatchFeatureScorer::addFeature(const FeatureVector& f) const {
+    assert(!bufferFilled());
+    setFeature(static_cast<size_t>(buffered_), f);
+    cached_[static_cast<size_t>(buffered_)] = 0;
+    ++buffered_;
+}
+
+// BatchFeatureScorerBase::getScorer, BatchFeatureScorer.cc:77-87
+Scorer GpuBatchFeatureScorer::getScorer(const FeatureVector& f) const {
+    assert(bufferFilled());
+    const int32_t b        = static_cast<int32_t>(bufferSize_);
+    const int32_t posToAdd = currentFeature_ ? (currentFeature_ - 1) % b : b - 1;
+    setFeature(static_cast<size_t>(posToAdd), f);
+    ++buffered_;
+    cached_[static_cast<size_t>(posToAdd)] = 0;  // invalidateCache(posToAdd)
+    Scorer result = std::make_shared<BufferedScorer>(this, currentFeature_, buffered_, assigning_);
+    currentFeature_ = (currentFeature_ + 1) % b;
+    --buffered_;
+    return result;
+}
+
+// BatchFeatureScorerBase::flush, BatchFeatureScorer.cc:89-96
+Scorer GpuBatchFeatureScorer::flush() const {
+    assert(buffered_ > 0 && !bufferEmpty());
+    Scorer result   = std::make_shared<BufferedScorer>(this, currentFeature_, buffered_, assigning_);
+    currentFeature_ = (currentFeature_ + 1) % static_cast<int32_t>(bufferSize_);
+    --buffered_;
+    return result;
+}
+
+// Score all mixtures of the buffered positions featureIndex .. featureIndex+length-1 (mod buffer)
+// in one launch and cache them (the reference's fillScoreCache does one mixture at a time).
+void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
+    const uint32_t b = bufferSize_;
+    length           = std::min(length, b);
+    for (uint32_t i = 0; i < length; ++i) {
+        const uint32_t p = (featureIndex + i) % b;
+        std::copy(features_.begin() + static_cast<size_t>(p) * dimension_,
+                  features_.begin() + static_cast<size_t>(p + 1) * dimension_,
+                  gather_.begin() + static_cast<size_t>(i) * dimension_);
+    }
+    ++launches_;
+    if (gmm_score_host(handle_, gather_.data(), length, dimension_, gatherScores_.data(),
+                       assigning_ ? gatherBest_.data() : nullptr, length) != GMM_OK)
+        return;
+    for (uint32_t i = 0; i < length; ++i) {
+        const uint32_t p = (featureIndex + i) % b;
+        for (uint32_t e = 0; e < nMixtures_; ++e) {
+            scores_[static_cast<size_t>(e) * b + p] = gatherScores_[static_cast<size_t>(e) * length + i];
+            if (assigning_)
+                best_[static_cast<size_t>(e) * b + p] = gatherBest_[static_cast<size_t>(e) * length + i];
+        }
+        cached_[p] = 1;
+    }
+}
+
+// BatchFeatureScorerBase::getScore, BatchFeatureScorer.cc:98-105
+Score GpuBatchFeatureScorer::getScore(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {
+    assert(e < nMixtures_);
+    const uint32_t p = featureIndex % bufferSize_;
+    if (!cached_[p])
+        fill(featureIndex, length);
+    return scores_[static_cast<size_t>(e) * bufferSize_ + p];
+}
+
+DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {
+    assert(e < nMixtures_);
+    const uint32_t p = featureIndex % bufferSize_;
+    if (!cached_[p])
+        fill(featureIndex, length);
+    return best_[static_cast<size_t>(e) * bufferSize_ + p];
+}
+
+// ---------------------------------------------------------------------------
+std::unique_ptr<FeatureScorer> createFeatureScorer(const MixtureSet& ms, const Configuration& c, std::string* error) {
+    gmm_scorer_type t;
+    bool            assigning = false, batch = false;
+    if (!typeOf(c.type, &t, &assigning, &batch)) {
+        if (error)
+            *error = "unknown feature scorer type: " + c.type;
+        return nullptr;
+    }
+    if (batch || c.bufferSize > 1)
+        return GpuBatchFeatureScorer::create(ms, c, error);
+    return GpuFeatureScorer::create(ms, c, error);
+}
+
+}  // namespace Gpu
+}  // namespace Mm

@@ -1,0 +1,178 @@
+// GpuFeatureScorer.hh -- host-side C++ mirror of RASR's feature-scorer plugin surface on top of
+// the MI355X C-ABI (include/rasr_gmm.h).
+//
+// Class and method names follow src/Mm/FeatureScorer.hh:28-164 (FeatureScorer, ContextScorer,
+// the buffered protocol isBuffered/addFeature/flush/bufferFilled/bufferEmpty/bufferSize/reset),
+// src/Mm/AssigningFeatureScorer.hh:29-48 (bestDensity) and src/Mm/BatchFeatureScorer.hh:34-199
+// (ring buffer semantics).  Core::Ref<const ContextScorer> becomes std::shared_ptr; Core
+// configuration parameters become a plain struct.  Inside an RASR build these classes are the
+// bodies of Mm::FeatureScorer subclasses (INTEGRATION.md shows the registration).
+//
+// Errors: the constructors never throw; create() returns nullptr and sets *error (the reference
+// calls criticalError(), src/Mm/Module.cc:305).  Methods keep the reference's require()
+// preconditions as assertions.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../../include/rasr_gmm.h"
+
+namespace Mm {
+namespace Gpu {
+
+typedef float                    Score;            // Mm::Score (src/Mm/Types.hh)
+typedef uint32_t                 EmissionIndex;    // Mm::EmissionIndex
+typedef uint32_t                 DensityInMixture; // Mm::DensityInMixture
+typedef std::vector<float>       FeatureVector;    // Mm::FeatureVector
+
+// ---------------------------------------------------------------------------
+// MixtureSet: the tables of Mm::MixtureSet the scorers read (src/Mm/MixtureSet.hh:140-212)
+// ---------------------------------------------------------------------------
+class MixtureSet {
+public:
+    explicit MixtureSet(uint32_t dimension) : dimension_(dimension) {}
+
+    uint32_t dimension() const { return dimension_; }
+    uint32_t nMixtures() const { return static_cast<uint32_t>(mixtureOffsets_.size() - 1); }
+    uint32_t nDensities() const { return static_cast<uint32_t>(densityMean_.size()); }
+
+    uint32_t addMean(const std::vector<float>& mean);                 // MixtureSet::addMean
+    uint32_t addCovariance(const std::vector<float>& diagonal);       // addCovariance(new DiagonalCovariance)
+    uint32_t addDensity(uint32_t meanIndex, uint32_t covarianceIndex); // addDensity(new GaussDensity(m, c))
+    // Mixture with its densities and log-weights (Mixture::addLogDensity, src/Mm/Mixture.hh:41)
+    uint32_t addMixture(const std::vector<uint32_t>& densities, const std::vector<double>& logWeights);
+
+    // descriptor of the C-ABI (valid while this object is alive and unchanged)
+    gmm_mixture_set descriptor() const;
+
+private:
+    uint32_t              dimension_;
+    std::vector<float>    means_, variances_;
+    std::vector<uint32_t> densityMean_, densityCovariance_;
+    std::vector<uint32_t> mixtureOffsets_{0}, mixtureDensities_;
+    std::vector<double>   mixtureLogWeights_;
+};
+
+// ---------------------------------------------------------------------------
+// ContextScorer: scores of one feature vector (FeatureScorer.hh:33-45, AssigningFeatureScorer.hh:36-48)
+// ---------------------------------------------------------------------------
+class ContextScorer {
+public:
+    virtual ~ContextScorer() {}
+    virtual EmissionIndex    nEmissions() const                 = 0;
+    virtual Score            score(EmissionIndex e) const       = 0;
+    virtual bool             hasBestDensity() const             { return false; }
+    virtual DensityInMixture bestDensity(EmissionIndex e) const { (void)e; return 0xffffffffu; }
+};
+typedef std::shared_ptr<const ContextScorer> Scorer;   // Core::Ref<const ContextScorer>
+
+struct Configuration {
+    std::string type               = "SIMD-diagonal-maximum";  // feature-scorer-type (src/Mm/Module.cc:78-80)
+    uint32_t    bufferSize         = 4;     // "buffer-size" (BatchFeatureScorer.cc:28-29)
+    float       mixtureWeightScale = 1.0f;  // "mixture-weight-scale" (GDMFS.cc:38-40)
+    float       gaussianScale      = 1.0f;  // "gaussian-scale" (GDMFS.cc:42-44)
+    float       scale              = 1.0f;  // FeatureScorerScaling scale (ScaledFeatureScorer.hh:62-64)
+    int         device             = 0;
+};
+
+// ---------------------------------------------------------------------------
+// FeatureScorer (src/Mm/FeatureScorer.hh:28-164)
+// ---------------------------------------------------------------------------
+class FeatureScorer {
+public:
+    virtual ~FeatureScorer();
+
+    EmissionIndex nMixtures() const { return nMixtures_; }
+    uint32_t      dimension() const { return dimension_; }
+
+    virtual Scorer getScorer(const FeatureVector& f) const = 0;
+    virtual void   reset() const {}
+    virtual void   finalize() const {}
+    virtual bool   isBuffered() const { return false; }
+    virtual void   addFeature(const FeatureVector& f) const { (void)f; }
+    virtual Scorer flush() const { return Scorer(); }
+    virtual bool   bufferFilled() const { return true; }
+    virtual bool   bufferEmpty() const { return true; }
+    virtual uint32_t bufferSize() const { return 0; }
+
+    // SimdGaussDiagonalMaximumFeatureScorer::inverseQuantizationFactor (SimdFeatureScorer.hh:128-130)
+    float inverseQuantizationFactor() const;
+    // SimdGaussDiagonalMaximumFeatureScorer::multiplyAndQuantize (SimdFeatureScorer.cc:37-52)
+    std::vector<std::vector<uint8_t>> multiplyAndQuantize(const FeatureVector& f) const;
+
+    gmm_scorer* handle() const { return handle_; }
+
+protected:
+    FeatureScorer() {}
+    bool init(const MixtureSet& ms, const Configuration& c, uint32_t maxFrames, std::string* error);
+
+    gmm_scorer*   handle_    = nullptr;
+    EmissionIndex nMixtures_ = 0;
+    uint32_t      dimension_ = 0;
+    bool          assigning_ = false;  // scorer type reports best densities
+    Configuration config_;
+};
+
+// Unbuffered scorer: every getScorer() scores one frame against all mixtures on the GPU
+// (the SIMD / diagonal-maximum scorers' Context, SimdFeatureScorer.cc:22-35).
+class GpuFeatureScorer : public FeatureScorer {
+public:
+    static std::unique_ptr<GpuFeatureScorer> create(const MixtureSet& ms, const Configuration& c,
+                                                     std::string* error = nullptr);
+    Scorer getScorer(const FeatureVector& f) const override;
+
+private:
+    GpuFeatureScorer() {}
+};
+
+// Buffered scorer: the BatchFeatureScorerBase ring-buffer protocol (BatchFeatureScorer.cc:40-116).
+// When a score of a buffered position is requested and not cached, ALL mixtures of all buffered
+// frames are scored in one GPU launch (the reference fills one mixture at a time).
+class GpuBatchFeatureScorer : public FeatureScorer {
+public:
+    static std::unique_ptr<GpuBatchFeatureScorer> create(const MixtureSet& ms, const Configuration& c,
+                                                          std::string* error = nullptr);
+    Scorer   getScorer(const FeatureVector& f) const override;
+    void     reset() const override;
+    bool     isBuffered() const override { return true; }
+    void     addFeature(const FeatureVector& f) const override;
+    Scorer   flush() const override;
+    bool     bufferFilled() const override { return buffered_ >= static_cast<int32_t>(bufferSize_) - 1; }
+    bool     bufferEmpty() const override { return buffered_ <= 0; }
+    uint32_t bufferSize() const override { return bufferSize_; }
+
+    Score            getScore(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
+    DensityInMixture getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
+
+    // number of GPU launches so far (tests check that one launch serves a whole buffer)
+    uint32_t nLaunches() const { return launches_; }
+
+private:
+    GpuBatchFeatureScorer() {}
+    void setFeature(size_t pos, const FeatureVector& f) const;
+    void fill(uint32_t featureIndex, uint32_t length) const;
+
+    uint32_t                      bufferSize_ = 4;
+    mutable std::vector<float>    features_;   // [bufferSize][dimension]
+    mutable std::vector<float>    scores_;     // [nMixtures][bufferSize] (BatchFeatureScorer.hh:177-186)
+    mutable std::vector<uint32_t> best_;       // [nMixtures][bufferSize]
+    mutable std::vector<char>     cached_;     // [bufferSize] (all mixtures of a position at once)
+    mutable std::vector<float>    gather_;     // staging for one launch
+    mutable std::vector<float>    gatherScores_;
+    mutable std::vector<uint32_t> gatherBest_;
+    mutable int32_t               currentFeature_ = 0;
+    mutable int32_t               buffered_       = 0;
+    mutable uint32_t              launches_       = 0;
+};
+
+// Factory by reference type name ("SIMD-diagonal-maximum", "diagonal-maximum",
+// "batch-diagonal-maximum-int", "batch-diagonal-maximum-float", "batch-diagonal-maximum-fast"):
+// batch-* types (and bufferSize > 1) give the buffered scorer.
+std::unique_ptr<FeatureScorer> createFeatureScorer(const MixtureSet& ms, const Configuration& c,
+                                                   std::string* error = nullptr);
+
+}  // namespace Gpu
+}  // namespace Mm

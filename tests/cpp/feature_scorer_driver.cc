@@ -1,0 +1,108 @@
+// feature_scorer_driver.cc -- drives Mm::Gpu::FeatureScorer exactly as RASR's recognizer does
+// (src/Speech/Recognizer.cc:198-206 leaveSpeechSegment, :272-282 processFeature) and dumps every
+// ContextScorer's scores, so tests/test_host_protocol.py can compare them with the oracle.
+//
+// usage: feature_scorer_driver <model.bin> <frames.bin> <out.bin> <type> <bufferSize> <segments>
+//   model.bin : u32 D, nMeans, nCov, nDens, nMix, nEntries; f32 means[nMeans*D]; f32 var[nCov*D];
+//               u32 densMean[nDens]; u32 densCov[nDens]; u32 offsets[nMix+1]; u32 dens[nEntries];
+//               f64 logw[nEntries]
+//   frames.bin: u32 F, D; f32 frames[F*D]
+//   out.bin   : u32 F, M, launches; f32 scores[F*M] (frame-major, as consumed); u32 best[F*M]
+// The frames are split into `segments` equal speech segments with reset() between them.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../rasr_amd/csrc/host/GpuFeatureScorer.hh"
+
+template <class T>
+static bool readVec(FILE* f, std::vector<T>& v, size_t n) {
+    v.resize(n);
+    return n == 0 || fread(v.data(), sizeof(T), n, f) == n;
+}
+
+int main(int argc, char** argv) {
+    if (argc != 7) {
+        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments\n", argv[0]);
+        return 2;
+    }
+    FILE* fm = fopen(argv[1], "rb");
+    FILE* ff = fopen(argv[2], "rb");
+    if (!fm || !ff)
+        return 2;
+    uint32_t h[6];
+    if (fread(h, sizeof(uint32_t), 6, fm) != 6)
+        return 2;
+    const uint32_t        D = h[0], nMeans = h[1], nCov = h[2], nDens = h[3], nMix = h[4], nEnt = h[5];
+    std::vector<float>    means, var;
+    std::vector<uint32_t> dm, dc, off, dens;
+    std::vector<double>   logw;
+    if (!readVec(fm, means, size_t(nMeans) * D) || !readVec(fm, var, size_t(nCov) * D) || !readVec(fm, dm, nDens) ||
+        !readVec(fm, dc, nDens) || !readVec(fm, off, nMix + 1) || !readVec(fm, dens, nEnt) || !readVec(fm, logw, nEnt))
+        return 2;
+    fclose(fm);
+    uint32_t fh[2];
+    if (fread(fh, sizeof(uint32_t), 2, ff) != 2 || fh[1] != D)
+        return 2;
+    std::vector<float> frames;
+    if (!readVec(ff, frames, size_t(fh[0]) * D))
+        return 2;
+    fclose(ff);
+    const uint32_t F = fh[0];
+
+    Mm::Gpu::MixtureSet ms(D);
+    for (uint32_t i = 0; i < nMeans; ++i)
+        ms.addMean(std::vector<float>(means.begin() + size_t(i) * D, means.begin() + size_t(i + 1) * D));
+    for (uint32_t c = 0; c < nCov; ++c)
+        ms.addCovariance(std::vector<float>(var.begin() + size_t(c) * D, var.begin() + size_t(c + 1) * D));
+    for (uint32_t i = 0; i < nDens; ++i)
+        ms.addDensity(dm[i], dc[i]);
+    for (uint32_t m = 0; m < nMix; ++m)
+        ms.addMixture(std::vector<uint32_t>(dens.begin() + off[m], dens.begin() + off[m + 1]),
+                      std::vector<double>(logw.begin() + off[m], logw.begin() + off[m + 1]));
+
+    Mm::Gpu::Configuration cfg;
+    cfg.type       = argv[4];
+    cfg.bufferSize = static_cast<uint32_t>(atoi(argv[5]));
+    std::string                             err;
+    std::unique_ptr<Mm::Gpu::FeatureScorer> scorer = Mm::Gpu::createFeatureScorer(ms, cfg, &err);
+    if (!scorer) {
+        fprintf(stderr, "createFeatureScorer failed: %s\n", err.c_str());
+        return 3;
+    }
+    const uint32_t        M = scorer->nMixtures();
+    std::vector<float>    outS;
+    std::vector<uint32_t> outB;
+    auto consume = [&](const Mm::Gpu::Scorer& s) {  // the search reads score(e) for active e
+        for (uint32_t e = 0; e < M; ++e) {
+            outS.push_back(s->score(e));
+            outB.push_back(s->hasBestDensity() ? s->bestDensity(e) : 0xffffffffu);
+        }
+    };
+    const uint32_t segments = static_cast<uint32_t>(atoi(argv[6]));
+    for (uint32_t seg = 0; seg < segments; ++seg) {
+        scorer->reset();
+        const uint32_t t0 = F * seg / segments, t1 = F * (seg + 1) / segments;
+        for (uint32_t t = t0; t < t1; ++t) {
+            Mm::Gpu::FeatureVector f(frames.begin() + size_t(t) * D, frames.begin() + size_t(t + 1) * D);
+            if (scorer->isBuffered() && !scorer->bufferFilled())  // Recognizer.cc:275-277
+                scorer->addFeature(f);
+            else
+                consume(scorer->getScorer(f));
+        }
+        if (scorer->isBuffered())  // Recognizer.cc:200-204
+            while (!scorer->bufferEmpty())
+                consume(scorer->flush());
+    }
+    uint32_t launches = 0;
+    if (auto* b = dynamic_cast<Mm::Gpu::GpuBatchFeatureScorer*>(scorer.get()))
+        launches = b->nLaunches();
+    FILE* fo = fopen(argv[3], "wb");
+    const uint32_t oh[3] = {static_cast<uint32_t>(outS.size() / (M ? M : 1)), M, launches};
+    fwrite(oh, sizeof(uint32_t), 3, fo);
+    fwrite(outS.data(), sizeof(float), outS.size(), fo);
+    fwrite(outB.data(), sizeof(uint32_t), outB.size(), fo);
+    fclose(fo);
+    return 0;
+}

@@ -1,0 +1,80 @@
+"""The C++ host-side scorer classes (rasr_amd/csrc/host/GpuFeatureScorer.hh) driven through the
+reference recognizer's protocol (tests/cpp/feature_scorer_driver.cc mirrors
+src/Speech/Recognizer.cc:198-206,272-282) against the oracle, frame by frame."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import rasr_amd as ra
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "build", "tests", "feature_scorer_driver")
+
+
+def _write_model(path, ms):
+    with open(path, "wb") as f:
+        np.array([ms.dimension, ms.means.shape[0], ms.n_covariances, ms.n_densities, ms.n_mixtures, ms.n_entries],
+                 dtype=np.uint32).tofile(f)
+        ms.means.astype(np.float32).tofile(f)
+        ms.variances.astype(np.float32).tofile(f)
+        ms.density_mean.astype(np.uint32).tofile(f)
+        ms.density_covariance.astype(np.uint32).tofile(f)
+        ms.mixture_offsets.astype(np.uint32).tofile(f)
+        ms.mixture_densities.astype(np.uint32).tofile(f)
+        ms.mixture_log_weights.astype(np.float64).tofile(f)
+
+
+def _run(tmp_path, ms, frames, kind, buffer_size, segments):
+    mp, fp, op = tmp_path / "m.bin", tmp_path / "f.bin", tmp_path / "o.bin"
+    _write_model(mp, ms)
+    with open(fp, "wb") as f:
+        np.array(frames.shape, dtype=np.uint32).tofile(f)
+        frames.astype(np.float32).tofile(f)
+    subprocess.run([DRIVER, str(mp), str(fp), str(op), kind, str(buffer_size), str(segments)], check=True,
+                   timeout=300)
+    raw = np.fromfile(op, dtype=np.uint32)
+    F, M, launches = raw[:3]
+    s = raw[3:3 + F * M].view(np.float32).reshape(F, M)
+    b = raw[3 + F * M:3 + 2 * F * M].reshape(F, M)
+    return s, b, int(launches)
+
+
+def test_driver_built(built):
+    assert os.access(DRIVER, os.X_OK)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("buffer_size", [1, 4, 7])
+def test_simd_protocol_bit_exact(gpu, tmp_path, buffer_size):
+    ms = ra.synthetic_mixture_set(30, 9, 39, seed=41, weights="random")
+    frames = ra.synthetic_frames(53, 39, seed=42)
+    s, b, launches = _run(tmp_path, ms, frames, "SIMD-diagonal-maximum", buffer_size, 3)
+    ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+    assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
+    assert np.array_equal(b.T, ref_b)
+    if buffer_size > 1:
+        assert launches <= 53  # a launch serves every buffered frame
+
+
+@pytest.mark.gpu
+def test_batch_int_protocol_bit_exact(gpu, tmp_path):
+    ms = ra.synthetic_mixture_set(25, 12, 39, seed=43)
+    frames = ra.synthetic_frames(40, 39, seed=44)
+    s, _, launches = _run(tmp_path, ms, frames, "batch-diagonal-maximum-int", 4, 2)
+    ref = oracle.batch_int_score(ms, frames)
+    assert np.array_equal(s.T.view(np.uint32), ref.view(np.uint32))
+    assert launches < 40
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["diagonal-maximum", "batch-diagonal-maximum-float"])
+def test_float_protocol(gpu, tmp_path, kind):
+    ms = ra.synthetic_mixture_set(25, 12, 45, seed=45, weights="random")
+    frames = ra.synthetic_frames(31, 45, seed=46)
+    s, _, _ = _run(tmp_path, ms, frames, kind, 4, 2)
+    ref = oracle.OracleFloat(ms).score(frames)[0] if kind == "diagonal-maximum" else oracle.batch_float_score(ms, frames)
+    err = np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))
+    assert err.max() <= 1e-4
