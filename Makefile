@@ -15,11 +15,11 @@ HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc
 HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh \
-            $(SRC)/host/GpuFeatureScorer.hh
+            $(SRC)/host/GpuFeatureScorer.hh include/rasr_gmm_io.h
 
 LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
-            $(BUILD)/GpuFeatureScorer.o
+            $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 all: $(LIB) $(DRIVER) oracle
@@ -44,9 +44,13 @@ $(BUILD)/GpuFeatureScorer.o: $(SRC)/host/GpuFeatureScorer.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	g++ $(HOSTFLAGS) -c $< -o $@
 
+$(BUILD)/MixtureSetFile.o: $(SRC)/host/MixtureSetFile.cc $(HDRS)
+	@mkdir -p $(BUILD)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz
 
 $(DRIVER): tests/cpp/feature_scorer_driver.cc $(LIB) $(HDRS)
 	@mkdir -p $(BUILD)/tests

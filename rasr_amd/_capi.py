@@ -64,7 +64,7 @@ class ScorerConfig(ctypes.Structure):
     ]
 
 
-# (name, restype, argtypes) for every function declared in include/rasr_gmm.h
+# (name, restype, argtypes) for every function declared in include/rasr_gmm.h and rasr_gmm_io.h
 PROTOTYPES = [
     ("gmm_default_config", None, [ctypes.POINTER(ScorerConfig)]),
     ("gmm_scorer_create", ctypes.c_int,
@@ -92,6 +92,13 @@ PROTOTYPES = [
     ("gmm_scorer_kernel_time", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), _u32p, ctypes.c_int]),
     ("gmm_last_error", ctypes.c_char_p, []),
+    # include/rasr_gmm_io.h
+    ("gmm_mixture_set_read", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(MixtureSetDesc)]),
+    ("gmm_mixture_set_parse", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(MixtureSetDesc)]),
+    ("gmm_mixture_set_free", ctypes.c_int, [ctypes.POINTER(MixtureSetDesc)]),
+    ("gmm_mixture_set_write", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MixtureSetDesc), ctypes.c_uint32]),
     ("gmm_version", ctypes.c_char_p, []),
 ]
 

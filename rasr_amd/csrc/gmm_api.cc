@@ -59,6 +59,13 @@ struct ChunkTable {
 
 }  // namespace
 
+namespace rasr_gmm {
+// shared with the other C-ABI translation units (host/MixtureSetFile.cc)
+void setLastError(const std::string& msg) {
+    gLastError = msg;
+}
+}  // namespace rasr_gmm
+
 struct gmm_scorer {
     gmm_scorer_type   type;
     Flavor            flavor;

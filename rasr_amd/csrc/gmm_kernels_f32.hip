@@ -73,7 +73,10 @@ __global__ __launch_bounds__(256) void prepareFramesF32(const float* __restrict_
 }
 
 template <int NF, int KS, bool MULTI>
-__global__ __launch_bounds__(256) void scoreF32(F32Args a) {
+#ifndef GMM_F32_MIN_WAVES
+#define GMM_F32_MIN_WAVES 1  // __launch_bounds__ minimum waves per SIMD (register budget)
+#endif
+__global__ __launch_bounds__(256, GMM_F32_MIN_WAVES) void scoreF32(F32Args a) {
     static_assert(NF == 4 || NF == 8, "NF");
     constexpr int NPL = NF / 4;
     const int     lane = threadIdx.x & 63;
@@ -158,19 +161,72 @@ __global__ __launch_bounds__(256) void scoreF32(F32Args a) {
                     for (int r = 0; r < 4; ++r)
                         best[cb][r] = fminf(best[cb][r], fminf(key(accA[cb][r], tl), key(accB[cb][r], tl + 1)));
             }
-            for (; t < tEnd;) {
+#if GMM_F32_DEFER
+            // software pipeline: the min/argmin epilogue of tile t-1 is issued together with the MFMA
+            // chain of tile t (independent registers), so the VALU work fills MFMA issue gaps instead
+            // of stalling the chain; unrolled by two so the two accumulator sets never move.
+            const auto epi = [&](const f32x4(&acc)[NF], uint32_t tl) {
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        best[cb][r] = fminf(best[cb][r], key(acc[cb][r], tl));
+            };
+            const auto advance = [&]() {
+#pragma unroll
+                for (int s = 0; s < KS; ++s)
+                    A0[s] = A1[s];
+                loadTile(t + 2, A1);
+                ++t;
+            };
+            if (t < tEnd) {
+                f32x4    accP[NF], accQ[NF];
+                uint32_t tlP = t - tBeg, tlQ = 0;
+                chain(A0, accP);
+                advance();
+                for (;;) {
+                    if (t >= tEnd) {
+                        epi(accP, tlP);
+                        break;
+                    }
+                    tlQ = t - tBeg;
+                    chain(A0, accQ);
+                    epi(accP, tlP);
+                    advance();
+                    if (t >= tEnd) {
+                        epi(accQ, tlQ);
+                        break;
+                    }
+                    tlP = t - tBeg;
+                    chain(A0, accP);
+                    epi(accQ, tlQ);
+                    advance();
+                }
+            }
+#endif
+            for (; !GMM_F32_DEFER && t < tEnd;) {
                 f32x4 accA[NF];
                 chain(A0, accA);
                 const uint32_t tl = t - tBeg;
+#if GMM_ABL_NO_EPI  // ablation build only: keep every chain alive, drop the per-element epilogue
+                float keep = 0.0f;
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+                    keep += accA[cb][0];
+                best[0][0] = fminf(best[0][0], key(keep, tl));
+#else
 #pragma unroll
                 for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         best[cb][r] = fminf(best[cb][r], key(accA[cb][r], tl));
+#endif
+#if !GMM_ABL_NO_LOAD  // ablation build only: reuse the first tile's operands
 #pragma unroll
                 for (int s = 0; s < KS; ++s)
                     A0[s] = A1[s];
                 loadTile(t + 2, A1);
+#endif
                 ++t;
             }
         }

@@ -36,6 +36,28 @@ uint32_t MixtureSet::addMixture(const std::vector<uint32_t>& densities, const st
     return nMixtures() - 1;
 }
 
+std::unique_ptr<MixtureSet> MixtureSet::read(const std::string& filename, std::string* error, uint32_t dimensionOffset,
+                                             uint32_t reducedDimension) {
+    gmm_mixture_set d;
+    if (gmm_mixture_set_read(filename.c_str(), dimensionOffset, reducedDimension, &d) != GMM_OK) {
+        if (error)
+            *error = gmm_last_error();
+        return nullptr;
+    }
+    std::unique_ptr<MixtureSet> ms(new MixtureSet(d.dimension));
+    const size_t                D = d.dimension;
+    ms->means_.assign(d.means, d.means + d.n_means * D);
+    ms->variances_.assign(d.variances, d.variances + d.n_covariances * D);
+    ms->densityMean_.assign(d.density_mean, d.density_mean + d.n_densities);
+    ms->densityCovariance_.assign(d.density_covariance, d.density_covariance + d.n_densities);
+    ms->mixtureOffsets_.assign(d.mixture_offsets, d.mixture_offsets + d.n_mixtures + 1);
+    const uint32_t nEntries = d.mixture_offsets[d.n_mixtures];
+    ms->mixtureDensities_.assign(d.mixture_densities, d.mixture_densities + nEntries);
+    ms->mixtureLogWeights_.assign(d.mixture_log_weights, d.mixture_log_weights + nEntries);
+    gmm_mixture_set_free(&d);
+    return ms;
+}
+
 gmm_mixture_set MixtureSet::descriptor() const {
     gmm_mixture_set d;
     std::memset(&d, 0, sizeof(d));

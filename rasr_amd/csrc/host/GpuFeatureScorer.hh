@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../../include/rasr_gmm.h"
+#include "../../../include/rasr_gmm_io.h"
 
 namespace Mm {
 namespace Gpu {
@@ -47,6 +48,11 @@ public:
 
     // descriptor of the C-ABI (valid while this object is alive and unchanged)
     gmm_mixture_set descriptor() const;
+
+    // Module_::readMixtureSet (src/Mm/Module.cc:152-182) for the text format (".pms", ".pms.gz"),
+    // via gmm_mixture_set_read (include/rasr_gmm_io.h); nullptr and *error on failure
+    static std::unique_ptr<MixtureSet> read(const std::string& filename, std::string* error,
+                                            uint32_t dimensionOffset = 0, uint32_t reducedDimension = 0);
 
 private:
     uint32_t              dimension_;

@@ -8,6 +8,7 @@ alive while the descriptor is used).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -83,6 +84,57 @@ class MixtureSet:
         z = np.load(path, allow_pickle=False)
         return MixtureSet(z["means"], z["variances"], z["density_mean"], z["density_covariance"],
                           z["mixture_offsets"], z["mixture_densities"], z["mixture_log_weights"])
+
+
+def _from_desc(d: _capi.MixtureSetDesc) -> MixtureSet:
+    def arr(ptr, n, dtype):
+        if n == 0:
+            return np.zeros(0, dtype=dtype)
+        return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+    D = int(d.dimension)
+    n_entries = int(d.mixture_offsets[d.n_mixtures]) if d.mixture_offsets else 0
+    return MixtureSet(
+        means=arr(d.means, d.n_means * D, np.float32).reshape(d.n_means, D),
+        variances=arr(d.variances, d.n_covariances * D, np.float32).reshape(d.n_covariances, D),
+        density_mean=arr(d.density_mean, d.n_densities, np.uint32),
+        density_covariance=arr(d.density_covariance, d.n_densities, np.uint32),
+        mixture_offsets=arr(d.mixture_offsets, d.n_mixtures + 1, np.uint32),
+        mixture_densities=arr(d.mixture_densities, n_entries, np.uint32),
+        mixture_log_weights=arr(d.mixture_log_weights, n_entries, np.float64))
+
+
+def read_mixture_set(path: str, dimension_offset: int = 0, reduced_dimension: int = 0) -> MixtureSet:
+    """Read a RASR ".pms" / ".pms.gz" text mixture set through the C-ABI
+    (gmm_mixture_set_read, include/rasr_gmm_io.h; Mm::Module_::readMixtureSet,
+    src/Mm/Module.cc:152-182, with the reduced-mixture-set-dimension[-offset] parameters)."""
+    lib = _capi.load_library()
+    d = _capi.MixtureSetDesc()
+    _capi.check(lib.gmm_mixture_set_read(os.fsencode(path), dimension_offset, reduced_dimension, ctypes.byref(d)),
+                "gmm_mixture_set_read")
+    try:
+        return _from_desc(d)
+    finally:
+        lib.gmm_mixture_set_free(ctypes.byref(d))
+
+
+def parse_mixture_set(data: bytes, dimension_offset: int = 0, reduced_dimension: int = 0) -> MixtureSet:
+    """gmm_mixture_set_parse: the same reader over in-memory (plain or gzip) bytes."""
+    lib = _capi.load_library()
+    d = _capi.MixtureSetDesc()
+    buf = ctypes.create_string_buffer(data, len(data))
+    _capi.check(lib.gmm_mixture_set_parse(buf, len(data), dimension_offset, reduced_dimension, ctypes.byref(d)),
+                "gmm_mixture_set_parse")
+    try:
+        return _from_desc(d)
+    finally:
+        lib.gmm_mixture_set_free(ctypes.byref(d))
+
+
+def write_mixture_set(path: str, ms: MixtureSet, precision: int = 6) -> None:
+    """gmm_mixture_set_write: MixtureSet::write text (src/Mm/MixtureSet.cc:142-168), gzip for *.gz."""
+    lib = _capi.load_library()
+    d = ms.desc()
+    _capi.check(lib.gmm_mixture_set_write(os.fsencode(path), ctypes.byref(d), precision), "gmm_mixture_set_write")
 
 
 def synthetic_mixture_set(n_mixtures: int, densities_per_mixture, dimension: int, seed: int = 1234,

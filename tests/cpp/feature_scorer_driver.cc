@@ -2,7 +2,8 @@
 // (src/Speech/Recognizer.cc:198-206 leaveSpeechSegment, :272-282 processFeature) and dumps every
 // ContextScorer's scores, so tests/test_host_protocol.py can compare them with the oracle.
 //
-// usage: feature_scorer_driver <model.bin> <frames.bin> <out.bin> <type> <bufferSize> <segments>
+// usage: feature_scorer_driver <model> <frames.bin> <out.bin> <type> <bufferSize> <segments>
+//   model     : a RASR mixture-set text file (*.pms, *.pms.gz; MixtureSet::read) or
 //   model.bin : u32 D, nMeans, nCov, nDens, nMix, nEntries; f32 means[nMeans*D]; f32 var[nCov*D];
 //               u32 densMean[nDens]; u32 densCov[nDens]; u32 offsets[nMix+1]; u32 dens[nEntries];
 //               f64 logw[nEntries]
@@ -22,26 +23,59 @@ static bool readVec(FILE* f, std::vector<T>& v, size_t n) {
     return n == 0 || fread(v.data(), sizeof(T), n, f) == n;
 }
 
-int main(int argc, char** argv) {
-    if (argc != 7) {
-        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments\n", argv[0]);
-        return 2;
-    }
-    FILE* fm = fopen(argv[1], "rb");
-    FILE* ff = fopen(argv[2], "rb");
-    if (!fm || !ff)
-        return 2;
+// the binary dump written by tests/test_host_protocol.py, built through the MixtureSet::add* API
+static std::unique_ptr<Mm::Gpu::MixtureSet> readBinaryModel(const std::string& path) {
+    FILE* fm = fopen(path.c_str(), "rb");
+    if (!fm)
+        return nullptr;
     uint32_t h[6];
     if (fread(h, sizeof(uint32_t), 6, fm) != 6)
-        return 2;
+        return nullptr;
     const uint32_t        D = h[0], nMeans = h[1], nCov = h[2], nDens = h[3], nMix = h[4], nEnt = h[5];
     std::vector<float>    means, var;
     std::vector<uint32_t> dm, dc, off, dens;
     std::vector<double>   logw;
     if (!readVec(fm, means, size_t(nMeans) * D) || !readVec(fm, var, size_t(nCov) * D) || !readVec(fm, dm, nDens) ||
         !readVec(fm, dc, nDens) || !readVec(fm, off, nMix + 1) || !readVec(fm, dens, nEnt) || !readVec(fm, logw, nEnt))
-        return 2;
+        return nullptr;
     fclose(fm);
+    std::unique_ptr<Mm::Gpu::MixtureSet> ms(new Mm::Gpu::MixtureSet(D));
+    for (uint32_t i = 0; i < nMeans; ++i)
+        ms->addMean(std::vector<float>(means.begin() + size_t(i) * D, means.begin() + size_t(i + 1) * D));
+    for (uint32_t c = 0; c < nCov; ++c)
+        ms->addCovariance(std::vector<float>(var.begin() + size_t(c) * D, var.begin() + size_t(c + 1) * D));
+    for (uint32_t i = 0; i < nDens; ++i)
+        ms->addDensity(dm[i], dc[i]);
+    for (uint32_t m = 0; m < nMix; ++m)
+        ms->addMixture(std::vector<uint32_t>(dens.begin() + off[m], dens.begin() + off[m + 1]),
+                       std::vector<double>(logw.begin() + off[m], logw.begin() + off[m + 1]));
+    return ms;
+}
+
+int main(int argc, char** argv) {
+    if (argc != 7) {
+        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments\n", argv[0]);
+        return 2;
+    }
+    const std::string modelPath(argv[1]);
+    const bool        pms = modelPath.size() > 4 && (modelPath.find(".pms") != std::string::npos);
+    FILE*             ff  = fopen(argv[2], "rb");
+    if (!ff)
+        return 2;
+    std::unique_ptr<Mm::Gpu::MixtureSet> model;
+    if (pms) {
+        std::string err;
+        model = Mm::Gpu::MixtureSet::read(modelPath, &err);
+        if (!model) {
+            fprintf(stderr, "MixtureSet::read failed: %s\n", err.c_str());
+            return 3;
+        }
+    }
+    else
+        model = readBinaryModel(modelPath);
+    if (!model)
+        return 2;
+    const uint32_t D = model->dimension();
     uint32_t fh[2];
     if (fread(fh, sizeof(uint32_t), 2, ff) != 2 || fh[1] != D)
         return 2;
@@ -51,17 +85,7 @@ int main(int argc, char** argv) {
     fclose(ff);
     const uint32_t F = fh[0];
 
-    Mm::Gpu::MixtureSet ms(D);
-    for (uint32_t i = 0; i < nMeans; ++i)
-        ms.addMean(std::vector<float>(means.begin() + size_t(i) * D, means.begin() + size_t(i + 1) * D));
-    for (uint32_t c = 0; c < nCov; ++c)
-        ms.addCovariance(std::vector<float>(var.begin() + size_t(c) * D, var.begin() + size_t(c + 1) * D));
-    for (uint32_t i = 0; i < nDens; ++i)
-        ms.addDensity(dm[i], dc[i]);
-    for (uint32_t m = 0; m < nMix; ++m)
-        ms.addMixture(std::vector<uint32_t>(dens.begin() + off[m], dens.begin() + off[m + 1]),
-                      std::vector<double>(logw.begin() + off[m], logw.begin() + off[m + 1]));
-
+    const Mm::Gpu::MixtureSet& ms = *model;
     Mm::Gpu::Configuration cfg;
     cfg.type       = argv[4];
     cfg.bufferSize = static_cast<uint32_t>(atoi(argv[5]));

@@ -27,9 +27,12 @@ def _write_model(path, ms):
         ms.mixture_log_weights.astype(np.float64).tofile(f)
 
 
-def _run(tmp_path, ms, frames, kind, buffer_size, segments):
+def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None):
     mp, fp, op = tmp_path / "m.bin", tmp_path / "f.bin", tmp_path / "o.bin"
-    _write_model(mp, ms)
+    if model_file is None:
+        _write_model(mp, ms)
+    else:
+        mp = model_file
     with open(fp, "wb") as f:
         np.array(frames.shape, dtype=np.uint32).tofile(f)
         frames.astype(np.float32).tofile(f)
@@ -78,3 +81,30 @@ def test_float_protocol(gpu, tmp_path, kind):
     ref = oracle.OracleFloat(ms).score(frames)[0] if kind == "diagonal-maximum" else oracle.batch_float_score(ms, frames)
     err = np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))
     assert err.max() <= 1e-4
+
+
+def test_driver_reads_pms_model(built, tmp_path):
+    """The driver's model path through MixtureSet::read: a broken .pms file is refused (exit 3)."""
+    bad = tmp_path / "bad.pms"
+    bad.write_text("#Version: 3.0\n#CovarianceType: DiagonalCovariance\n1 0 0 0 0\n")
+    fp = tmp_path / "f.bin"
+    with open(fp, "wb") as f:
+        np.array([1, 1], dtype=np.uint32).tofile(f)
+        np.zeros(1, np.float32).tofile(f)
+    r = subprocess.run([DRIVER, str(bad), str(fp), str(tmp_path / "o.bin"), "SIMD-diagonal-maximum", "1", "1"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3 and "not supported" in r.stderr
+
+
+@pytest.mark.gpu
+def test_simd_protocol_model_from_pms_file(gpu, tmp_path):
+    """OfflineRecognizer protocol with the model loaded from a .pms.gz file by the C++ host side."""
+    src = ra.synthetic_mixture_set(20, 7, 39, seed=47, weights="random", n_covariances=3)
+    path = tmp_path / "model.pms.gz"
+    ra.write_mixture_set(str(path), src, 6)
+    ms = ra.read_mixture_set(str(path))  # the model as the file holds it
+    frames = ra.synthetic_frames(33, 39, seed=48)
+    s, b, _ = _run(tmp_path, ms, frames, "SIMD-diagonal-maximum", 5, 2, model_file=path)
+    ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+    assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
+    assert np.array_equal(b.T, ref_b)
