@@ -11,6 +11,8 @@ I8FLAGS   = -mllvm -amdgpu-mfma-vgpr-form
 # float kernels: default AGPR accumulators (measured faster for the f32 MFMA chains) and one
 # tile per loop step (GMM_F32_PAIR=0), see DESIGN.md "Measurements"
 F32FLAGS  = -DGMM_F32_PAIR=0
+# split-f16 float kernel
+SPLITFLAGS =
 HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc
@@ -18,7 +20,7 @@ HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC
             $(SRC)/host/GpuFeatureScorer.hh include/rasr_gmm_io.h
 
 LIB       = $(LIBDIR)/librasr_gmm.so
-OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
+OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
             $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
@@ -31,6 +33,10 @@ $(BUILD)/gmm_kernels_i8.o: $(SRC)/gmm_kernels_i8.hip $(HDRS)
 $(BUILD)/gmm_kernels_f32.o: $(SRC)/gmm_kernels_f32.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(F32FLAGS) -c $< -o $@
+
+$(BUILD)/gmm_kernels_split.o: $(SRC)/gmm_kernels_split.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(SPLITFLAGS) -c $< -o $@
 
 $(BUILD)/gmm_api.o: $(SRC)/gmm_api.cc $(HDRS)
 	@mkdir -p $(BUILD)

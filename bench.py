@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--dim", type=int, default=39)
     p.add_argument("--no-best", action="store_true", help="do not write best-density indices")
     p.add_argument("--no-extra-mode", action="store_true", help="do not time the other mode")
+    p.add_argument("--native-f32", action="store_true",
+                   help="fp32 mode on the f32-MFMA kernel instead of the split-f16 kernel")
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-frames-per-thread", type=int, default=3000)
@@ -124,7 +126,8 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
         sc = scorer.scorer
         seed = 1000  # every rank scores the same frames
     else:
-        sc = ra.Scorer(ms, kind, max_frames=frames_per_gpu, device=local)
+        sc = ra.Scorer(ms, kind, max_frames=frames_per_gpu, device=local,
+                       native_f32=args.native_f32 and mode == "fp32")
         seed = 1000 + rank
     m_local = sc.n_mixtures()
     frames = torch.from_numpy(ra.synthetic_frames(frames_per_gpu, args.dim, seed=seed)).to(dev)

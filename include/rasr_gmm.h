@@ -67,8 +67,13 @@ typedef struct {
     uint32_t max_frames;           /* largest n_frames of one gmm_score_* call ("buffer-size", cc:28-29)         */
     uint32_t mixture_begin;        /* mixture shard [begin, end) scored by this handle; 0,0 = all mixtures        */
     uint32_t mixture_end;
-    uint32_t flags;                /* reserved, 0                                                                 */
+    uint32_t flags;                /* GMM_FLAG_* bits, 0 = defaults                                               */
 } gmm_scorer_config;
+
+/* Float types (diagonal-maximum, batch-float) with one covariance run on the f16
+ * matrix cores with every f32 operand split into two f16 pieces (f32 accuracy
+ * class); this flag selects the f32-MFMA kernel instead. */
+#define GMM_FLAG_NATIVE_F32 1u
 
 typedef struct gmm_scorer gmm_scorer;
 

@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RASR_GMM_LIB") or os.path.join(_HERE, "lib", "librasr_gmm.so")
 
 GMM_OK = 0
+GMM_FLAG_NATIVE_F32 = 1  # gmm_scorer_config.flags
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0

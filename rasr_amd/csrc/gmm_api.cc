@@ -76,6 +76,8 @@ struct gmm_scorer {
     uint32_t          nFramesPad = 0;
     bool              multiCov   = false;
     bool              foldNorm   = false;
+    bool              split      = false;  // float types on the split-f16 kernel
+    uint32_t          kSteps16   = 0;
     uint32_t          tileBits   = 1;
     float             offsetK0   = 0;
     // quantized scalars
@@ -95,6 +97,10 @@ struct gmm_scorer {
     int32_t* dFrameSS = nullptr;
     float*   dFrameX  = nullptr;
     float*   dFrameXX = nullptr;
+    void*    dFrameH  = nullptr;   // split kernel
+    int32_t* dFrameExp = nullptr;
+    float*   dDimScale = nullptr;
+    int32_t* dLimbExp  = nullptr;
     // host-API staging
     float*    dHostFrames = nullptr;
     float*    dHostScores = nullptr;
@@ -106,8 +112,9 @@ struct gmm_scorer {
     size_t                                      eventsUsed = 0;
 
     ~gmm_scorer() {
-        void* ptrs[] = {dTileA,  dTileP,  dTileCov, dRowDns,     dMixTileOff, dIsv,     dFrameQ,
-                        dFrameSS, dFrameX, dFrameXX, dHostFrames, dHostScores, dHostBest};
+        void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
+                        dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
+                        dFrameExp, dDimScale, dLimbExp};
         for (void* p : ptrs)
             if (p)
                 (void)hipFree(p);
@@ -124,7 +131,7 @@ struct gmm_scorer {
 namespace {
 
 uint32_t framesPerBlock(const gmm_scorer* s) {
-    return s->quantized ? kI8FramesPerBlock : kF32FramesPerBlock;
+    return s->quantized ? kI8FramesPerBlock : (s->split ? kSplitFramesPerBlock : kF32FramesPerBlock);
 }
 
 // Cut the shard's mixtures into chunks of about equal tile count so that
@@ -229,6 +236,34 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         GMM_HIP_CHECK(launchScoreI8(a, s->kSteps, s->multiCov, stream));
+        GMM_HIP_CHECK(span.end());
+    }
+    else if (s->split) {
+        GMM_HIP_CHECK(launchPrepareFramesSplit(frames, nFrames, frameStride, nPadCall, s->D, s->kSteps16, s->dIsv,
+                                               s->dDimScale, s->dLimbExp, s->dFrameH, s->dFrameXX, s->dFrameExp,
+                                               stream));
+        SplitArgs a{};
+        a.tileH       = s->dTileA;
+        a.mixTileOff  = s->dMixTileOff;
+        a.chunkMixOff = ct->dMixOff;
+        a.frameH      = s->dFrameH;
+        a.frameXX     = s->dFrameXX;
+        a.frameExp    = s->dFrameExp;
+        a.scores      = scores;
+        a.best        = s->flavor == Flavor::DiagonalMaximum ? best : nullptr;
+        a.nFrames     = nFrames;
+        a.nFramesPad  = s->nFramesPad;
+        a.scoreStride = scoreStride;
+        a.nChunks     = ct->nChunks;
+        a.nFrameTiles = nFrameTiles;
+        a.mixBase     = 0;
+        a.flavor      = s->flavor == Flavor::DiagonalMaximum ? 2 : 3;
+        a.tileBits    = s->tileBits;
+        a.offsetK0    = s->offsetK0;
+        a.outScale    = s->cfg.score_scale;
+        TimedSpan span(s, stream);
+        GMM_HIP_CHECK(span.begin());
+        GMM_HIP_CHECK(launchScoreSplit(a, s->kSteps16, stream));
         GMM_HIP_CHECK(span.end());
     }
     else {
@@ -361,9 +396,12 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     }
     else {
         PreparedFloat p;
-        std::string   err = prepareFloat(*ms, flavor, cfg.mixture_weight_scale, cfg.gaussian_scale, shard, p);
+        std::string   err = prepareFloat(*ms, flavor, cfg.mixture_weight_scale, cfg.gaussian_scale, shard, p,
+                                         (cfg.flags & GMM_FLAG_NATIVE_F32) == 0);
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
+        s->split    = p.split;
+        s->kSteps16 = p.kSteps16;
         s->nMix       = p.nMixtures;
         s->kSteps     = p.kSteps;
         s->multiCov   = s->C > 1;
@@ -372,6 +410,24 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         s->offsetK0   = p.offsetK0;
         s->nTiles     = p.tiling.nTiles;
         s->mixTileOff = p.tiling.mixTileOffset;
+        if (s->split) {
+            const std::vector<int32_t> limbs(p.limbExp, p.limbExp + kSplitLimbs);
+            const size_t               nH = static_cast<size_t>(s->nFramesPad) * p.kSteps16 * 32;
+            if ((rc = upload(reinterpret_cast<uint16_t**>(&s->dTileA), p.tileH, kTilePad * kLanes * 8 * p.kSteps16)) ||
+                (rc = upload(&s->dDimScale, p.dimScale)) || (rc = upload(&s->dLimbExp, limbs)) ||
+                (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)))
+                return rc;
+            GMM_HIP_CHECK(hipMalloc(&s->dFrameH, nH * sizeof(uint16_t)));
+            GMM_HIP_CHECK(hipMemset(s->dFrameH, 0, nH * sizeof(uint16_t)));
+            GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameXX), s->nFramesPad * sizeof(float)));
+            GMM_HIP_CHECK(hipMemset(s->dFrameXX, 0, s->nFramesPad * sizeof(float)));
+            GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameExp), s->nFramesPad * sizeof(int32_t)));
+            GMM_HIP_CHECK(hipMemset(s->dFrameExp, 0, s->nFramesPad * sizeof(int32_t)));
+            s->mixBase = shard.begin == 0 && shard.end == 0 ? 0 : shard.begin;
+            GMM_HIP_CHECK(hipDeviceSynchronize());
+            *out = s.release();
+            return GMM_OK;
+        }
         if ((rc = upload(reinterpret_cast<float**>(&s->dTileA), p.tileA, kTilePad * kLanes * p.kSteps)) ||
             (rc = upload(&s->dTileCov, p.tiling.tileCovariance, kTilePad)) ||
             (rc = upload(&s->dRowDns, p.tiling.rowDensityInMixture, kTilePad * kTileRows)) ||
@@ -513,7 +569,7 @@ int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLau
     if (nLaunches)
         *nLaunches = 2;
     if (name)
-        *name = s->quantized ? "scoreI8" : "scoreF32";
+        *name = s->quantized ? "scoreI8" : (s->split ? "scoreSplit" : "scoreF32");
     return GMM_OK;
 }
 

@@ -56,12 +56,46 @@ struct F32Args {
     float           outScale;
 };
 
+#ifndef GMM_SPLIT_NF
+#define GMM_SPLIT_NF 4
+#endif
+constexpr int      kSplitNF             = GMM_SPLIT_NF;  // column blocks of 16 frames per wave, split kernel
+constexpr uint32_t kSplitFramesPerBlock = kWavesPerBlock * kSplitNF * 16;
+
+constexpr uint32_t kSplitLimbs = 4;
+// K layout of the split kernel: [0,D) mh*xh, [D,2D) mh*xl, [2D,3D) ml*xh, [3D,3D+4) limbs
+inline uint32_t splitKSteps(uint32_t dimension) {
+    return (3 * dimension + kSplitLimbs + 31) / 32;
+}
+
+struct SplitArgs {
+    const void*     tileH;        // f16 [T+pad][KS16][64][8]
+    const uint32_t* mixTileOff;
+    const uint32_t* chunkMixOff;
+    const void*     frameH;       // f16 [nFramesPad/16][KS16][64][8]
+    const float*    frameXX;      // [nFramesPad]  ||x'||^2 * 2^-e
+    const int32_t*  frameExp;     // [nFramesPad]  e
+    float*          scores;
+    uint32_t*       best;
+    uint32_t        nFrames, nFramesPad, scoreStride;
+    uint32_t        nChunks, nFrameTiles, mixBase;
+    int             flavor;       // 2 diagonal-maximum, 3 batch-float
+    uint32_t        tileBits;
+    float           offsetK0;
+    float           outScale;
+};
+
 hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
                                  uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, const float* isv, int8_t* frameQ,
                                  int32_t* frameSS, hipStream_t stream);
 hipError_t launchPrepareFramesF32(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
                                   uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, int foldNorm, const float* isv, float* frameX,
                                   float* frameXX, hipStream_t stream);
+hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
+                                    uint32_t D, uint32_t KS16, const float* isv, const float* dimScale,
+                                    const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
+                                    hipStream_t stream);
+hipError_t launchScoreSplit(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream);
 hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 hipError_t launchScoreF32(const F32Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 

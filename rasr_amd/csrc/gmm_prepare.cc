@@ -315,7 +315,7 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
 // ---------------------------------------------------------------------------
 
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
-                         ShardRange shard, PreparedFloat& out) {
+                         ShardRange shard, PreparedFloat& out, bool wantSplit) {
     std::string err = validate(ms);
     if (!err.empty())
         return err;
@@ -387,33 +387,130 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
             return "float scorer supports at most 4096 densities per mixture";  // key precision 2^-15
     }
 
-    out.tileA.assign(static_cast<size_t>(T) * KS * kLanes, 0.0f);
-    std::vector<float> row(KS * 4);
-    for (uint32_t t = 0; t < T; ++t) {
-        for (uint32_t r = 0; r < kTileRows; ++r) {
-            const uint32_t e = out.tiling.rowEntry[static_cast<size_t>(t) * kTileRows + r];
-            std::fill(row.begin(), row.end(), 0.0f);
-            if (e == UINT32_MAX) {
-                row[D] = FLT_MAX;  // padding row: bias +FLT_MAX never wins a strict minimum
-            }
-            else {
-                const uint32_t dns  = ms.mixture_densities[e];
-                const uint32_t cov  = ms.density_covariance[dns];
-                const float*   mean = ms.means + static_cast<size_t>(ms.density_mean[dns]) * D;
-                const float*   iv   = out.isv.data() + static_cast<size_t>(cov) * D;
-                double         mm   = 0;
-                for (uint32_t k = 0; k < D; ++k) {
-                    const float mp = mean[k] * iv[k];
-                    row[k]         = -2.0f * mp;
-                    mm += static_cast<double>(mp) * mp;
+    // one row of the contraction: m2[k] = -2 m'_k (f32, as the native kernel's operand) and the
+    // row constant ||m'||^2 + c_d + K0 (f64); false for a padding row
+    const auto rowValues = [&](uint32_t t, uint32_t r, float* m2, double& cst) -> bool {
+        const uint32_t e = out.tiling.rowEntry[static_cast<size_t>(t) * kTileRows + r];
+        if (e == UINT32_MAX)
+            return false;
+        const uint32_t dns  = ms.mixture_densities[e];
+        const uint32_t cov  = ms.density_covariance[dns];
+        const float*   mean = ms.means + static_cast<size_t>(ms.density_mean[dns]) * D;
+        const float*   iv   = out.isv.data() + static_cast<size_t>(cov) * D;
+        double         mm   = 0;
+        for (uint32_t k = 0; k < D; ++k) {
+            const float mp = mean[k] * iv[k];
+            m2[k]          = -2.0f * mp;
+            mm += static_cast<double>(mp) * mp;
+        }
+        cst = mm + rowConstant(e) + out.offsetK0;
+        return true;
+    };
+    std::vector<float> m2(D);
+    double             cst = 0;
+
+    // ---- split-f16 layout ----
+    if (wantSplit && !out.foldNorm && splitKSteps(D) <= 8 && T > 0) {
+        std::vector<double> maxAbs(D, 0.0);
+        double              maxConst = 0;
+        for (uint32_t t = 0; t < T; ++t)
+            for (uint32_t r = 0; r < kTileRows; ++r)
+                if (rowValues(t, r, m2.data(), cst)) {
+                    for (uint32_t k = 0; k < D; ++k)
+                        maxAbs[k] = std::max(maxAbs[k], std::fabs(static_cast<double>(m2[k])));
+                    maxConst = std::max(maxConst, std::fabs(cst));
                 }
-                row[D] = static_cast<float>(mm + rowConstant(e) + out.offsetK0);
-                if (out.foldNorm)
-                    row[D + 1] = 1.0f;
+        bool finite = std::isfinite(maxConst);
+        for (double v : maxAbs)
+            finite = finite && std::isfinite(v);
+        // limbs at 2^b0, 2^(b0-11), 2^(b0-22), 2^(b0-33): f16 frame-side multipliers need
+        // b0 <= 15 and b0 - 33 >= -24; limb 0 must hold const / 2^b0 <= 2^15
+        int b0 = 9;
+        while (b0 < 15 && maxConst / std::ldexp(1.0, b0) > 32768.0)
+            ++b0;
+        if (finite && maxConst / std::ldexp(1.0, b0) <= 32768.0) {
+            out.split    = true;
+            out.kSteps16 = splitKSteps(D);
+            for (uint32_t s = 0; s < kSplitLimbs; ++s)
+                out.limbExp[s] = b0 - 11 * static_cast<int32_t>(s);
+            // per-dimension power of two that puts max|m''_d| in [2^7, 2^8): m'' and x'' then sit in
+            // the middle of the f16 range for frames of the model's own scale
+            out.dimScale.assign(D, 1.0f);
+            std::vector<double> inv(D, 1.0);
+            for (uint32_t k = 0; k < D; ++k)
+                if (maxAbs[k] > 0) {
+                    int ex;
+                    std::frexp(maxAbs[k], &ex);  // maxAbs in [2^(ex-1), 2^ex)
+                    const int a     = std::max(-60, std::min(60, ex - 1 - 7));
+                    out.dimScale[k] = static_cast<float>(std::ldexp(1.0, a));
+                    inv[k]          = std::ldexp(1.0, -a);
+                }
+            const auto h16 = [](double v) {
+                const _Float16 h = static_cast<_Float16>(v);  // round to nearest even, one rounding
+                uint16_t       b;
+                std::memcpy(&b, &h, 2);
+                return b;
+            };
+            const auto f16v = [](uint16_t b) {
+                _Float16 h;
+                std::memcpy(&h, &b, 2);
+                return static_cast<double>(h);
+            };
+            const uint32_t KS16 = out.kSteps16;
+            out.tileH.assign(static_cast<size_t>(T) * KS16 * kLanes * 8, 0);
+            std::vector<uint16_t> row(KS16 * 32);
+            for (uint32_t t = 0; t < T; ++t) {
+                for (uint32_t r = 0; r < kTileRows; ++r) {
+                    std::fill(row.begin(), row.end(), 0);
+                    // a padding row repeats row 0 of its tile (every tile starts with a real row):
+                    // an exact tie with a lower density index never wins, and no +inf/NaN keys
+                    if (rowValues(t, r, m2.data(), cst) || rowValues(t, 0, m2.data(), cst)) {
+                        for (uint32_t k = 0; k < D; ++k) {
+                            const float    v  = static_cast<float>(m2[k] * inv[k]);  // exact: power of two
+                            const uint16_t hi = h16(v);
+                            const uint16_t lo = h16(static_cast<double>(v) - f16v(hi));
+                            row[k]            = hi;
+                            row[D + k]        = hi;
+                            row[2 * D + k]    = lo;
+                        }
+                        double rem = cst;
+                        for (uint32_t s = 0; s < kSplitLimbs; ++s) {
+                            const uint16_t l = h16(std::ldexp(rem, -out.limbExp[s]));
+                            row[3 * D + s]   = l;
+                            rem -= std::ldexp(f16v(l), out.limbExp[s]);
+                        }
+                    }
+                    // fragment order of v_mfma_f32_16x16x32_f16: lane = 16*((k>>3)&3) + row, step k>>5
+                    for (uint32_t k = 0; k < KS16 * 32; ++k) {
+                        const uint32_t lane = 16 * ((k >> 3) & 3) + r;
+                        out.tileH[((static_cast<size_t>(t) * KS16 + (k >> 5)) * kLanes + lane) * 8 + (k & 7)] = row[k];
+                    }
+                }
             }
-            // fragment order of v_mfma_f32_16x16x4_f32: lane = 16*(k&3) + row, step s = k>>2
-            for (uint32_t k = 0; k < KS * 4; ++k)
-                out.tileA[(static_cast<size_t>(t) * KS + k / 4) * kLanes + (k % 4) * 16 + r] = row[k];
+        }
+    }
+
+    // ---- native f32 layout ----
+    if (!out.split) {
+        out.tileA.assign(static_cast<size_t>(T) * KS * kLanes, 0.0f);
+        std::vector<float> row(KS * 4);
+        for (uint32_t t = 0; t < T; ++t) {
+            for (uint32_t r = 0; r < kTileRows; ++r) {
+                std::fill(row.begin(), row.end(), 0.0f);
+                if (!rowValues(t, r, m2.data(), cst)) {
+                    row[D] = FLT_MAX;  // padding row: bias +FLT_MAX never wins a strict minimum
+                }
+                else {
+                    for (uint32_t k = 0; k < D; ++k)
+                        row[k] = m2[k];
+                    row[D] = static_cast<float>(cst);
+                    if (out.foldNorm)
+                        row[D + 1] = 1.0f;
+                }
+                // fragment order of v_mfma_f32_16x16x4_f32: lane = 16*(k&3) + row, step s = k>>2
+                for (uint32_t k = 0; k < KS * 4; ++k)
+                    out.tileA[(static_cast<size_t>(t) * KS + k / 4) * kLanes + (k % 4) * 16 + r] = row[k];
+            }
         }
     }
     out.isvDevice.assign(static_cast<size_t>(C) * KS * 4, 0.0f);

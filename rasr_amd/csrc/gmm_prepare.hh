@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/rasr_gmm.h"
+#include "gmm_kernels.hh"
 
 namespace rasr_gmm {
 
@@ -87,9 +88,17 @@ struct PreparedFloat {
     std::vector<float> isv;           // [C][dimension] (after gaussian-scale)
     std::vector<float> logNorm;       // [C]
     Tiling             tiling;
-    std::vector<float> tileA;         // [nTiles][kSteps][64 lanes]
+    std::vector<float> tileA;         // [nTiles][kSteps][64 lanes]  (empty when split)
     std::vector<float> isvDevice;     // [C][kSteps*4] zero padded
+    // split-f16 kernel (single covariance, gmm_kernels_split.hip): every f32 operand is a sum of
+    // two f16 pieces, hi + lo; a row is  sum_d [mh*xh + mh*xl + ml*xh]  +  sum_s limb_s * 2^(b_s)
+    bool                  split    = false;
+    uint32_t              kSteps16 = 0;    // K/32 steps of v_mfma_f32_16x16x32_f16
+    std::vector<uint16_t> tileH;           // [nTiles][kSteps16][64 lanes][8] f16 bits
+    std::vector<float>    dimScale;        // [dimension]: 2^a_d, x'' = x' * 2^a_d, m'' = -2 m' / 2^a_d
+    int32_t               limbExp[4] = {0, 0, 0, 0};  // b_s: the frame side of limb s is 2^(b_s - e_frame)
 };
+
 
 struct ShardRange {
     uint32_t begin = 0, end = 0;
@@ -98,7 +107,9 @@ struct ShardRange {
 // Returns empty string on success, else an error message.
 std::string validate(const gmm_mixture_set& ms);
 std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out);
+// wantSplit: lay the model out for the split-f16 kernel when it applies (one covariance,
+// 3*dimension+4 <= 256, row constants below 2^30); out.split says whether it did.
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
-                         ShardRange shard, PreparedFloat& out);
+                         ShardRange shard, PreparedFloat& out, bool wantSplit = false);
 
 }  // namespace rasr_gmm

@@ -30,7 +30,7 @@ class Scorer:
 
     def __init__(self, mixture_set: MixtureSet, scorer_type="SIMD-diagonal-maximum", max_frames: int = 4096,
                  device: int = 0, mixture_weight_scale: float = 1.0, gaussian_scale: float = 1.0,
-                 score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None):
+                 score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None, native_f32: bool = False):
         self._lib = _capi.load_library()
         self.mixture_set = mixture_set
         self.type = _type_id(scorer_type)
@@ -39,6 +39,8 @@ class Scorer:
         cfg.mixture_weight_scale = mixture_weight_scale
         cfg.gaussian_scale = gaussian_scale
         cfg.score_scale = score_scale
+        if native_f32:  # float types: the f32-MFMA kernel instead of the split-f16 one
+            cfg.flags |= _capi.GMM_FLAG_NATIVE_F32
         if mixture_range is not None:
             cfg.mixture_begin, cfg.mixture_end = int(mixture_range[0]), int(mixture_range[1])
         self.max_frames = int(max_frames)
@@ -63,6 +65,14 @@ class Scorer:
     @property
     def handle(self):
         return self._h
+
+    def main_kernel(self) -> str:
+        """Name of the dominant kernel a score call launches (gmm_scorer_launch_info)."""
+        n = ctypes.c_uint32()
+        name = ctypes.c_char_p()
+        _capi.check(self._lib.gmm_scorer_launch_info(self._h, 1, ctypes.byref(n), ctypes.byref(name)),
+                    "gmm_scorer_launch_info")
+        return name.value.decode()
 
     def n_mixtures(self) -> int:
         return int(self._lib.gmm_scorer_n_mixtures(self._h))

@@ -1,19 +1,21 @@
 #!/bin/bash
 # Build kernel variants for A/B timing (scripts/ab_bench.py):
 #   build_variants.sh <name> "<i8 kernel flags>" "<f32 kernel flags>" [<name> "<i8>" "<f32>"]...
+# (the f32 flags also go to the split-f16 kernel TU; -D flags reach gmm_api.cc too)
 # -> rasr_amd/lib/variants/librasr_gmm_<name>.so (same host objects, different kernel objects)
 set -e
 cd "$(dirname "$0")/.."
-make -s build/gmm_api.o build/gmm_prepare.o
+make -s build/gmm_api.o build/gmm_prepare.o build/GpuFeatureScorer.o build/MixtureSetFile.o
 mkdir -p rasr_amd/lib/variants build/variants
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off"
 while [ $# -ge 3 ]; do
   name=$1; i8=$2; f32=$3; shift 3
   /opt/rocm/bin/hipcc $BASE $i8 -c rasr_amd/csrc/gmm_kernels_i8.hip -o build/variants/i8_$name.o
   /opt/rocm/bin/hipcc $BASE $f32 -c rasr_amd/csrc/gmm_kernels_f32.hip -o build/variants/f32_$name.o
+  /opt/rocm/bin/hipcc $BASE $f32 -c rasr_amd/csrc/gmm_kernels_split.hip -o build/variants/split_$name.o
   defs=$(echo "$i8 $f32" | tr ' ' '\n' | grep '^-D' | tr '\n' ' ')
   /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -ffp-contract=off $defs -c rasr_amd/csrc/gmm_api.cc -o build/variants/api_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o rasr_amd/lib/variants/librasr_gmm_$name.so \
-      build/variants/i8_$name.o build/variants/f32_$name.o build/variants/api_$name.o build/gmm_prepare.o
+      build/variants/i8_$name.o build/variants/f32_$name.o build/variants/split_$name.o build/variants/api_$name.o build/gmm_prepare.o build/GpuFeatureScorer.o build/MixtureSetFile.o -lz
   echo built $name
 done
