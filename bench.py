@@ -39,7 +39,9 @@ sys.path.insert(0, ROOT)
 
 # gfx950 peaks (MI355X_MICROARCH.md, chip-level parameters / matrix cores)
 PEAK_F32_MFMA_TFLOPS = 157.3          # v_mfma_f32_16x16x4_f32, dense
+PEAK_F16_MFMA_TFLOPS = 2516.6         # v_mfma_f32_16x16x32_f16, dense (same rate as bf16)
 PEAK_I8_MFMA_TOPS = 2 * 2516.6        # i8 MFMA = 2x the bf16 dense rate
+SPLIT_PRODUCTS = 3                    # split-f16 kernel: mh*xh + mh*xl + ml*xh per f32 multiply-add
 
 MODES = {
     "fp32": ("diagonal-maximum", "f32"),
@@ -158,12 +160,27 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
     d_local = int(ms.mixture_offsets[min(ms.n_mixtures, scorer.shards[rank][1])]
                   - ms.mixture_offsets[scorer.shards[rank][0]]) if sharded else int(ms.n_entries)
     algo = 2.0 * args.dim * d_local * frames_per_gpu  # one multiply-add per (frame, density, component)
-    peak = PEAK_F32_MFMA_TFLOPS if mode == "fp32" else PEAK_I8_MFMA_TOPS
-    achieved = algo / (kms_avg * 1e-3) / 1e12
+    kernel = sc.main_kernel()
+    if kernel == "scoreSplit":
+        # f32-accurate contraction on the f16 matrix cores: 3 f16 products per f32 multiply-add, so the
+        # roofline for this arithmetic is the dense f16 peak / 3; the MFMA work actually issued covers
+        # K = 32 * ceil((3 D + 4) / 32) per (frame, density) (row constant limbs + padding)
+        peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PRODUCTS
+        k_issued = 32 * ((3 * args.dim + 4 + 31) // 32)
+        issued = 2.0 * k_issued * d_local * frames_per_gpu
+    elif mode == "fp32":
+        peak = PEAK_F32_MFMA_TFLOPS
+        issued = 2.0 * 4 * ((args.dim + 1 + 3) // 4) * d_local * frames_per_gpu
+    else:
+        peak = PEAK_I8_MFMA_TOPS
+        issued = 2.0 * 64 * ((args.dim + 63) // 64) * d_local * frames_per_gpu
+    sec = kms_avg * 1e-3
+    achieved = algo / sec / 1e12
     res = {
         "value": total_frames / dt_max,
         "ms_per_step": dt_max / args.steps * 1e3,
-        "dtype": dtype,
+        "dtype": dtype if kernel != "scoreSplit" else
+        "f32 (operands split into 2 f16 pieces, 3 f16 MFMA products, f32 accumulate)",
         "frames_per_gpu": frames_per_gpu,
         "roofline": {
             "bound": "mfma",
@@ -172,9 +189,13 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
             "unit": "TFLOP/s",
             "frac": achieved / peak,
             "traffic": load_pmc(mode) if not sharded else None,
-            "kernel": "scoreI8Seg" if mode == "simd" else "scoreF32",
+            "kernel": kernel,
             "kernel_ms": kms_avg,
             "algorithmic_flop_per_launch": algo,
+            "issued_mfma_flop_per_launch": issued,
+            "issued_mfma_tflops": issued / sec / 1e12,
+            "issued_mfma_frac_of_dtype_peak": issued / sec / 1e12 / (
+                PEAK_F16_MFMA_TFLOPS if kernel == "scoreSplit" else peak),
             "output_bytes_per_launch": m_local * frames_per_gpu * (4 + (0 if best is None else 4)),
         },
     }

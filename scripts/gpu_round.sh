@@ -16,14 +16,18 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-STEPS=${STEPS:-"pytest smoke bench_fp32 bench_simd prof"}
+STEPS=${STEPS:-"pytest smoke bench_fp32 bench_simd prof pmc"}
 for s in $STEPS; do
   case $s in
     pytest) step pytest 1200 python -m pytest tests -x -q -m gpu ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_fp32) step bench_fp32 600 python bench.py --mode fp32 --steps 20 --warmup 3 ;;
     bench_simd) step bench_simd 600 python bench.py --mode simd --steps 20 --warmup 3 --cpu-baseline off ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --mode fp32 --steps 10 --warmup 2 --cpu-baseline off --extra-mode ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --mode fp32 --steps 10 --warmup 2 --cpu-baseline off ;;
+    pmc) step pmc_fp32 900 bash scripts/profile_pmc.sh fp32 &&
+         step pmc_simd 900 bash scripts/profile_pmc.sh simd &&
+         python scripts/pmc_summary.py $OUT/pmc_fp32 scoreSplit --json $OUT/pmc_fp32.json > /dev/null &&
+         python scripts/pmc_summary.py $OUT/pmc_simd scoreI8 --json $OUT/pmc_simd.json > /dev/null ;;
   esac
 done
 echo done
