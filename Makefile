@@ -12,7 +12,7 @@ I8FLAGS   = -mllvm -amdgpu-mfma-vgpr-form
 # tile per loop step (GMM_F32_PAIR=0), see DESIGN.md "Measurements"
 F32FLAGS  = -DGMM_F32_PAIR=0
 # split-f16 float kernel
-SPLITFLAGS =
+SPLITFLAGS = -mllvm -amdgpu-mfma-vgpr-form
 HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc

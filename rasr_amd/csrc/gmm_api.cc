@@ -406,7 +406,7 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         s->kSteps     = p.kSteps;
         s->multiCov   = s->C > 1;
         s->foldNorm   = p.foldNorm;
-        s->tileBits   = p.tileBits;
+        s->tileBits   = p.split ? p.splitKeyBits : p.tileBits;  // split kernel: key bits
         s->offsetK0   = p.offsetK0;
         s->nTiles     = p.tiling.nTiles;
         s->mixTileOff = p.tiling.mixTileOffset;

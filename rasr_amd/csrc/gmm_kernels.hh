@@ -57,15 +57,19 @@ struct F32Args {
 };
 
 #ifndef GMM_SPLIT_NF
-#define GMM_SPLIT_NF 4
+#define GMM_SPLIT_NF 4  // the split kernel is written for 4 (emitMixtureSplit)
 #endif
 constexpr int      kSplitNF             = GMM_SPLIT_NF;  // column blocks of 16 frames per wave, split kernel
 constexpr uint32_t kSplitFramesPerBlock = kWavesPerBlock * kSplitNF * 16;
 
-constexpr uint32_t kSplitLimbs = 4;
-// K layout of the split kernel: [0,D) mh*xh, [D,2D) mh*xl, [2D,3D) ml*xh, [3D,3D+4) limbs
+constexpr uint32_t kSplitLimbs   = 4;
+constexpr uint32_t kSplitXXLimbs = 3;
+// the frame's ||x'||^2 rides in K as three f16 limbs against these powers of two on the model side
+constexpr int kSplitXXExp[kSplitXXLimbs] = {15, 4, -7};
+// K layout of the split kernel: [0,D) mh*xh, [D,2D) mh*xl, [2D,3D) ml*xh, [3D,3D+4) row-constant
+// limbs, [3D+4,3D+7) ||x'||^2 limbs
 inline uint32_t splitKSteps(uint32_t dimension) {
-    return (3 * dimension + kSplitLimbs + 31) / 32;
+    return (3 * dimension + kSplitLimbs + kSplitXXLimbs + 31) / 32;
 }
 
 struct SplitArgs {

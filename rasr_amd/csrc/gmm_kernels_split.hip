@@ -26,7 +26,8 @@
 // tile bits would be a signalling NaN, which v_min_f32 turns into a quiet NaN result).
 //
 // K layout (host and frame preparation agree): [0,D) mh.xh, [D,2D) mh.xl, [2D,3D) ml.xh,
-// [3D,3D+4) limbs, rest zero.  Fragment order of v_mfma_f32_16x16x32_f16: lane l holds
+// [3D,3D+4) row-constant limbs, [3D+4,3D+7) limbs of the frame's ||x'||^2 2^-e (against 2^15,
+// 2^4, 2^-7 on the model side), rest zero.  Fragment order of v_mfma_f32_16x16x32_f16: lane l holds
 // A[row l&15][k = 8(l>>4) + j] and B[k = 8(l>>4) + j][col l&15], j = 0..7; C/D hold
 // col l&15, rows 4(l>>4) + r.
 //
@@ -35,12 +36,6 @@
 // minimum is a float key whose low tileBits mantissa bits hold the tile number.
 #include "gmm_device.hh"
 
-#ifndef GMM_SPLIT_PAIR
-#define GMM_SPLIT_PAIR 1  // two tiles per loop step, v_min3 over both
-#endif
-#ifndef GMM_SPLIT_EMIT_OLD
-#define GMM_SPLIT_EMIT_OLD 0  // A/B only: per-candidate lexMin with validity branches at mixture end
-#endif
 #ifndef GMM_SPLIT_MIN_WAVES
 #define GMM_SPLIT_MIN_WAVES 1
 #endif
@@ -50,6 +45,10 @@ namespace dev {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t umin3(uint32_t x, uint32_t y, uint32_t z) {
+    return min(min(x, y), z);  // v_min3_u32
+}
 
 __device__ __forceinline__ uint16_t h16bits(float v) {
     const _Float16 h = static_cast<_Float16>(v);
@@ -89,8 +88,25 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
         frexpf(ymax, &ex);  // ymax in [2^(ex-1), 2^ex)
         e = ex - 15;
     }
-    frameXX[f]  = ldexpf(xx, -e);
-    frameExp[f] = e;
+    if (finite && xx < 3.40282347e+38f && ldexpf(xx, -e) >= 1073741824.0f) {  // ||x'||^2 2^-e < 2^30 (its top limb)
+        int ex;
+        frexpf(xx, &ex);
+        e = ex - 30;
+    }
+    const float xxs = ldexpf(xx, -e);
+    frameXX[f]      = xxs;
+    frameExp[f]     = e;
+    // ||x'||^2 2^-e as three f16 limbs against 2^15, 2^4, 2^-7 on the model side
+    uint16_t xxl[kSplitXXLimbs];
+    {
+        float rem = xxs;
+#pragma unroll
+        for (uint32_t s = 0; s < kSplitXXLimbs; ++s) {
+            xxl[s]         = h16bits(ldexpf(rem, -kSplitXXExp[s]));
+            const float lv = ldexpf(static_cast<float>(__builtin_bit_cast(_Float16, xxl[s])), kSplitXXExp[s]);
+            rem            = __fsub_rn(rem, lv);
+        }
+    }
     const uint32_t fb = f >> 4, col = f & 15;
     for (uint32_t q = 0; q < KS16 * 4; ++q) {  // groups of 8 consecutive k
         uint32_t w[4] = {0, 0, 0, 0};
@@ -108,6 +124,10 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
                     const int be = limbExp[k - 3 * D] - e;
                     h            = be < -24 ? 0 : h16bits(ldexpf(1.0f, be));
                 }
+                else if (k < 3 * D + kSplitLimbs + kSplitXXLimbs) {
+                    const uint32_t s = k - 3 * D - kSplitLimbs;
+                    h                = s == 0 ? xxl[0] : (s == 1 ? xxl[1] : xxl[2]);
+                }
                 w[j >> 1] |= static_cast<uint32_t>(h) << (16 * (j & 1));
             }
         // step q>>2, lane group q&3
@@ -116,98 +136,93 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
 }
 
 // ---------------------------------------------------------------------------
-// end of a mixture: the (value | tile) keys of the 4 row slots -> (score, density) per frame,
-// reduced across the four 16-lane groups by permlane swaps; lane l stores frame frame0 + 64 i + l
+// keys: a row's value v > 0 (row constants shifted by K0, ||x'||^2 the initial accumulator) is kept
+// as the u32 bits of the float with the low keyBits mantissa bits replaced by (tile << 2 | r), r the
+// accumulator slot (row 4g + r of the tile in lane group g).  Positive floats order like their bits,
+// so one v_and_or_b32 per value and one v_min3_u32 per two values keep, per lane and slot, the
+// minimum by (value, tile); the lane group g is resolved at the end of the mixture, where keys
+// equal in value and tag prefer the lower group (lower density index).
 // ---------------------------------------------------------------------------
-template <int NF>
-__device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, float* __restrict__ scores,
-                                                 uint32_t* __restrict__ bestOut, const float (&best)[NF][4],
-                                                 uint32_t m, uint32_t frame0, int lane, int g, uint32_t tmask,
-                                                 const int (&eOut)[NF / 4]) {
-    constexpr int NPL = NF / 4;
-    float         v[NF];   // key (value | tile) of the lane's best row slot
-    uint32_t      vi[NF];  // its density in the mixture: tile * 16 + 4 g + r
-#if GMM_SPLIT_EMIT_OLD
+
+// end of a mixture: the 4 slot keys of each column block -> (score, density) per frame, reduced
+// across the four 16-lane groups by permlane swaps (r0 of a swap always comes from the lower group);
+// lane l stores frame frame0 + l
+__device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][4], uint32_t m,
+                                                 uint32_t frame0, int lane, uint32_t g, uint32_t kmask, int eOut) {
+    uint32_t k[4];
 #pragma unroll
-    for (int cb = 0; cb < NF; ++cb) {
-        v[cb]  = 3.40282347e+38f;
-        vi[cb] = 0xffffffffu;
+    for (int cb = 0; cb < 4; ++cb)
+        k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
+    // groups {g&1, g&1|2} of blocks (0,2) and (1,3): lanes < 32 keep blocks 0, 1, lanes >= 32 blocks 2, 3
+    uint32_t w[2], wg[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t bits = __float_as_uint(best[cb][r]);
-            if (!(__uint_as_float(bits & ~tmask) < 1e37f))  // no finite candidate in this row slot
-                continue;
-            lexMin(v[cb], vi[cb], best[cb][r], (bits & tmask) * 16u + 4u * g + r);
-        }
+    for (int p = 0; p < 2; ++p) {
+        const auto     r    = __builtin_amdgcn_permlane32_swap(k[p], k[p + 2], false, false);
+        const bool     take = r[1] < r[0];
+        w[p]                = take ? r[1] : r[0];
+        wg[p]               = (g & 1u) | (take ? 2u : 0u);
     }
-#else
-    // branch-free: within a lane the keys order by (value, tile), so the minimum key and the first
-    // row slot holding it give the lexicographic (value, density) minimum; an empty slot keeps
-    // FLT_MAX, which loses to every finite key and is caught after the lane reduction
-#pragma unroll
-    for (int cb = 0; cb < NF; ++cb) {
-        const float k0 = best[cb][0], k1 = best[cb][1], k2 = best[cb][2], k3 = best[cb][3];
-        const float mn = fminf(fminf(k0, k1), fminf(k2, k3));
-        uint32_t    r  = k2 == mn ? 2u : 3u;
-        r              = k1 == mn ? 1u : r;
-        r              = k0 == mn ? 0u : r;
-        v[cb]          = mn;
-        vi[cb]         = ((__float_as_uint(mn) & tmask) << 4) | (4u * g + r);
+    // groups {even, odd} rows: lane l keeps block l >> 4
+    const auto     rk   = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
+    const auto     rg   = __builtin_amdgcn_permlane16_swap(wg[0], wg[1], false, false);
+    const bool     take = rk[1] < rk[0];
+    const uint32_t key  = take ? rk[1] : rk[0];
+    const uint32_t grp  = take ? rg[1] : rg[0];
+
+    const uint32_t f = frame0 + static_cast<uint32_t>(lane);
+    // midpoint of the masked bits: within 2^-(24 - keyBits) of the minimum's value
+    const float kv = __uint_as_float((key & ~kmask) | ((kmask + 1u) >> 1));
+    float       score;
+    uint32_t    idx;
+    if (!(kv < 1e37f)) {  // no finite candidate (empty mixture, non-finite frame): Core::Type<Score>::max
+        idx   = 0xffffffffu;
+        score = a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f;
     }
-#endif
-    float    w[NF / 2];
-    uint32_t wi[NF / 2];
-#pragma unroll
-    for (int p = 0; p < NF / 2; ++p) {
-        const int c = (p & 1) | ((p >> 1) << 2);
-        swapLexMin32(v[c], vi[c], v[c ^ 2], vi[c ^ 2], w[p], wi[p]);
+    else {
+        idx                = (((key & kmask) >> 2) << 4) | (grp << 2) | (key & 3u);
+        const float scaled = ldexpf(kv, eOut);
+        const float total  = a.offsetK0 != 0.0f ? __fsub_rn(scaled, a.offsetK0) : scaled;
+        score              = a.flavor == 2 ? 0.5f * total : (total < 3.40282347e+38f ? 0.5f * total : total);
     }
-    const uint32_t mo = m - a.mixBase;
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-        float    kv;
-        uint32_t ki;
-        swapLexMin16(w[2 * i], wi[2 * i], w[2 * i + 1], wi[2 * i + 1], kv, ki);
-        const uint32_t f = frame0 + 64 * i + lane;
-        if (f >= a.nFrames)
-            continue;
-        kv = __uint_as_float(__float_as_uint(kv) & ~tmask);
-        if (!(kv < 1e37f))  // no finite candidate at all (empty mixture, or non-finite frame)
-            ki = 0xffffffffu;
-        float score;
-        if (ki == 0xffffffffu) {  // no density: bestScore stays Core::Type<Score>::max
-            score = a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f;
-        }
-        else {
-            const float scaled = ldexpf(kv, eOut[i]);
-            const float total  = a.offsetK0 != 0.0f ? __fsub_rn(scaled, a.offsetK0) : scaled;
-            score              = a.flavor == 2 ? 0.5f * total : (total < 3.40282347e+38f ? 0.5f * total : total);
-        }
-        if (a.outScale != 1.0f)
-            score = __fmul_rn(a.outScale, score);
-        const size_t o = static_cast<size_t>(mo) * a.scoreStride + f;
-        scores[o]      = score;
-        if (bestOut)
-            bestOut[o] = ki;
+    if (a.outScale != 1.0f)
+        score = __fmul_rn(a.outScale, score);
+    const size_t o = static_cast<size_t>(m - a.mixBase) * a.scoreStride + f;
+    if (f < a.nFrames) {
+        a.scores[o] = score;
+        if (a.best)
+            a.best[o] = idx;
     }
 }
 
 // ---------------------------------------------------------------------------
-// scorer
+// scorer.  A workgroup = 4 waves x 64 frames (4 column blocks of 16) walks a chunk of mixtures on one
+// XCD.  Every mixture has an even number of tiles (host), so the chunk is a flat sequence of tile
+// pairs; the loop body takes two pairs, whose operands live in two named register sets (R0,R1 and
+// R2,R3) loaded two pairs ahead.  Mixture bounds are scalar loads (mixTileOff is a restrict kernel
+// argument): a vector load there would come with an s_waitcnt vmcnt(0) draining the prefetch and the
+// previous mixture's stores.
 // ---------------------------------------------------------------------------
-template <int NF, int KS>
-__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a) {
-    static_assert(NF == 4 || NF == 8, "NF");
-    const int     lane = threadIdx.x & 63;
-    const int     wave = threadIdx.x >> 6;
-    const int     g    = lane >> 4;
-    uint32_t      chunk, ft;
+template <int KS>
+__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
+                                                                      const uint32_t* __restrict__ mixTileOff) {
+    constexpr int  NF   = 4;
+    const int      lane = threadIdx.x & 63;
+    const int      wave = threadIdx.x >> 6;
+    const uint32_t g    = static_cast<uint32_t>(lane) >> 4;
+    uint32_t       chunk, ft;
     if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
         return;
     const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
     const uint32_t fb0    = frame0 / 16u;
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
 
+    const f16x8* th       = static_cast<const f16x8*>(a.tileH);
+    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS]) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+    };
     const f16x8* fh = static_cast<const f16x8*>(a.frameH);
     f16x8        B[NF][KS];
 #pragma unroll
@@ -215,250 +230,99 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs
 #pragma unroll
         for (int s = 0; s < KS; ++s)
             B[cb][s] = fh[(static_cast<size_t>(fb0 + cb) * KS + s) * 64 + lane];
-    f32x4 XX[NF];
+    const int eOut = a.frameExp[frame0 + lane];  // exponent of the frame this lane stores
+    // wait for the frame operands here, before the tile prefetch is issued: otherwise the waitcnt pass
+    // sees them possibly pending at the loop header and drains the whole queue there every iteration
 #pragma unroll
     for (int cb = 0; cb < NF; ++cb) {
-        const float xx = a.frameXX[frame0 + cb * 16 + (lane & 15)];
-        XX[cb]         = f32x4{xx, xx, xx, xx};
-    }
-    int eOut[NF / 4];  // frame exponents of the frames this lane stores (no vector load inside the loop)
-#pragma unroll
-    for (int i = 0; i < NF / 4; ++i)
-        eOut[i] = a.frameExp[frame0 + 64 * i + lane];
-
-    const f16x8* th = static_cast<const f16x8*>(a.tileH);
-    uint32_t     t  = a.mixTileOff[m0];
-    f16x8        A0[KS], A1[KS];
-    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS]) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-            A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+            asm volatile("" ::"v"(B[cb][s]));
+    }
+    asm volatile("" ::"v"(eOut));
+
+    // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
+    f16x8 R0[KS], R1[KS], R2[KS], R3[KS];
+    loadTile(T0, R0);
+    loadTile(T0 + 1, R1);
+    loadTile(T0 + 2, R2);
+    loadTile(T0 + 3, R3);
+
+    const uint32_t kmask = (1u << a.tileBits) - 1u;
+    // the value mask lives in a VGPR so that (bits & mask) | tag is ONE v_and_or_b32 with the tag in an
+    // SGPR (gfx950 VOP3 reads at most one SGPR)
+    uint32_t vmask = ~kmask;
+    asm volatile("" : "+v"(vmask));
+
+    uint32_t   best[NF][4];
+    const auto resetBest = [&]() {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                best[cb][r] = 0xffffffffu;
     };
-    loadTile(t, A0);
-    loadTile(t + 1, A1);
     const auto chain = [&](const f16x8(&A)[KS], f32x4(&acc)[NF]) {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
-            acc[cb] = XX[cb];
+            acc[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};  // ||x'||^2 is in K: the chain starts from an inline 0
 #pragma unroll
         for (int s = 0; s < KS; ++s)
 #pragma unroll
             for (int cb = 0; cb < NF; ++cb)
                 acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
     };
-    const uint32_t tmask = (1u << a.tileBits) - 1u;
-    // the value mask lives in a VGPR so that (bits & mask) | tile is ONE v_and_or_b32 (gfx950 VOP3 reads
-    // at most one SGPR; mask and tile number both in SGPRs would split it into v_and + v_or)
-    uint32_t vmask = ~tmask;
-    asm volatile("" : "+v"(vmask));
-    const auto key = [&](float v, uint32_t tl) { return __uint_as_float((__float_as_uint(v) & vmask) | tl); };
-
-    for (uint32_t m = m0; m < m1; ++m) {
-        const uint32_t tBeg = t, tEnd = a.mixTileOff[m + 1];
-        float          best[NF][4];
+    // one pair of tiles (tile numbers tl, tl + 1 in the mixture)
+    const auto pairStep = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], uint32_t tl) {
+        f32x4 accA[NF], accB[NF];
+        chain(A0, accA);
+        chain(A1, accB);
+        // per-slot tags as opaque SGPRs: with a visible constant the compiler splits the tag OR off the
+        // v_and_or_b32 into a v_and + v_or3 pair
+        uint32_t tagA[4], tagB[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            tagA[r] = (tl << 2) | r;
+            tagB[r] = ((tl + 1u) << 2) | r;
+            asm volatile("" : "+s"(tagA[r]), "+s"(tagB[r]));
+        }
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                best[cb][r] = 3.40282347e+38f;
-
-        for (; GMM_SPLIT_PAIR && t + 1 < tEnd; t += 2) {
-            f32x4 accA[NF], accB[NF];
-            chain(A0, accA);
-            loadTile(t + 2, A0);
-            chain(A1, accB);
-            loadTile(t + 3, A1);
-            const uint32_t tl = t - tBeg;
-#pragma unroll
-            for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    best[cb][r] = fminf(best[cb][r], fminf(key(accA[cb][r], tl), key(accB[cb][r], tl + 1)));
-        }
-        for (; t < tEnd; ++t) {
-            f32x4 acc[NF];
-            chain(A0, acc);
-            const uint32_t tl = t - tBeg;
-#pragma unroll
-            for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    best[cb][r] = fminf(best[cb][r], key(acc[cb][r], tl));
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-                A0[s] = A1[s];
-            loadTile(t + 2, A1);
-        }
-
-        emitMixtureSplit<NF>(a, a.scores, a.best, best, m, frame0, lane, g, tmask, eOut);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// scorer, tiles staged through LDS (the i8 kernel's segment ring, gmm_kernels_i8.hip): the four
-// waves of a workgroup walk the same tiles, so each 8-tile segment (8 x KS KiB) is brought into
-// LDS once by global_load_lds_dwordx4 (each wave issues a quarter of it) one segment ahead, and
-// every wave reads its A fragments with ds_read_b128; one global request per tile and workgroup
-// instead of one per wave, and eight tiles of latency hiding instead of two
-// ---------------------------------------------------------------------------
-constexpr int kSplitSegTiles = 8;
-
-template <int NF, int KS>
-__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplitSeg(SplitArgs a,
-                                                                         const uint32_t* __restrict__ mixTileOff,
-                                                                         float* __restrict__ scores,
-                                                                         uint32_t* __restrict__ bestOut) {
-    static_assert(NF == 4 || NF == 8, "NF");
-    constexpr uint32_t kTileA    = KS * 1024;  // operand bytes per tile
-    constexpr uint32_t kSegBytes = kSplitSegTiles * kTileA;
-    constexpr int      kPieces   = kSplitSegTiles * KS / 4;  // 1 KiB pieces per wave per segment
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kSegBytes];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int g    = lane >> 4;
-    uint32_t  chunk, ft;
-    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
-        return;  // uniform over the workgroup, before any barrier
-    const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
-    const uint32_t fb0    = frame0 / 16u;
-    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
-    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
-    const uint32_t nSeg = (T1 - T0 + kSplitSegTiles - 1) / kSplitSegTiles;
-    const uint8_t* gA   = static_cast<const uint8_t*>(a.tileH);
-
-    // segment s -> buffer (s & 1); the tile array is padded by kTilePad >= kSplitSegTiles tiles
-    const auto issueSeg = [&](uint32_t s) {
-        const uint32_t t0   = T0 + s * kSplitSegTiles;
-        uint8_t*       base = lds + (s & 1u) * kSegBytes;
-#pragma unroll
-        for (int i = 0; i < kPieces; ++i) {
-            const uint32_t piece = static_cast<uint32_t>(wave * kPieces + i);
-            __builtin_amdgcn_global_load_lds(gA + static_cast<size_t>(t0) * kTileA + piece * 1024u + lane * 16,
-                                             base + piece * 1024u, 16, 0, 0);
-        }
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t ka = (__float_as_uint(accA[cb][r]) & vmask) | tagA[r];
+                const uint32_t kb = (__float_as_uint(accB[cb][r]) & vmask) | tagB[r];
+                best[cb][r]       = umin3(best[cb][r], ka, kb);
+            }
     };
-    if (nSeg > 0)
-        issueSeg(0);
-    if (nSeg > 1)
-        issueSeg(1);
 
-    const f16x8* fh = static_cast<const f16x8*>(a.frameH);
-    f16x8        B[NF][KS];
-#pragma unroll
-    for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-            B[cb][s] = fh[(static_cast<size_t>(fb0 + cb) * KS + s) * 64 + lane];
-    f32x4 XX[NF];
-#pragma unroll
-    for (int cb = 0; cb < NF; ++cb) {
-        const float xx = a.frameXX[frame0 + cb * 16 + (lane & 15)];
-        XX[cb]         = f32x4{xx, xx, xx, xx};
-    }
-    int eOut[NF / 4];  // frame exponents of the frames this lane stores (no vector load inside the loop)
-#pragma unroll
-    for (int i = 0; i < NF / 4; ++i)
-        eOut[i] = a.frameExp[frame0 + 64 * i + lane];
-    const uint32_t tmask = (1u << a.tileBits) - 1u;
-    // the value mask lives in a VGPR so that (bits & mask) | tile is ONE v_and_or_b32 (gfx950 VOP3 reads
-    // at most one SGPR; mask and tile number both in SGPRs would split it into v_and + v_or)
-    uint32_t vmask = ~tmask;
-    asm volatile("" : "+v"(vmask));
-    const auto key = [&](float v, uint32_t tl) { return __uint_as_float((__float_as_uint(v) & vmask) | tl); };
-
-    float      best[NF][4];
-    const auto resetBest = [&]() {
-#pragma unroll
-        for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                best[cb][r] = 3.40282347e+38f;
-    };
+    uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
-    uint32_t m = m0, tBeg = T0, tEnd = mixTileOff[m0 + 1];
-    while (m < m1 && tEnd == T0) {  // mixtures without tiles at the start of the chunk
-        emitMixtureSplit<NF>(a, scores, bestOut, best, m, frame0, lane, g, tmask, eOut);
-        ++m;
-        tEnd = m < m1 ? mixTileOff[m + 1] : T1;
-    }
-
-    for (uint32_t s = 0; s < nSeg; ++s) {
-        // this segment's pieces (issued one segment ago) have landed; the next segment's stay in flight
-        if (s + 1 < nSeg)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPieces) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        const uint8_t* base   = lds + (s & 1u) * kSegBytes;
-        const uint32_t segT0  = T0 + s * kSplitSegTiles;
-        const uint32_t segEnd = min(segT0 + kSplitSegTiles, T1);
-        uint32_t       t      = segT0;
-        while (t < segEnd) {
-            const uint32_t lt = t - segT0;
-            const uint32_t tl = t - tBeg;
-            if (GMM_SPLIT_PAIR && t + 1 < segEnd && t + 1 < tEnd) {
-                f16x8 A0[KS], A1[KS];
-#pragma unroll
-                for (int k = 0; k < KS; ++k) {
-                    A0[k] = *reinterpret_cast<const f16x8*>(base + lt * kTileA + k * 1024 + lane * 16);
-                    A1[k] = *reinterpret_cast<const f16x8*>(base + (lt + 1) * kTileA + k * 1024 + lane * 16);
-                }
-                f32x4 accA[NF], accB[NF];
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb) {
-                    accA[cb] = XX[cb];
-                    accB[cb] = XX[cb];
-                }
-#pragma unroll
-                for (int k = 0; k < KS; ++k)
-#pragma unroll
-                    for (int cb = 0; cb < NF; ++cb) {
-                        accA[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[k], B[cb][k], accA[cb], 0, 0, 0);
-                        accB[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[k], B[cb][k], accB[cb], 0, 0, 0);
-                    }
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        best[cb][r] = fminf(best[cb][r], fminf(key(accA[cb][r], tl), key(accB[cb][r], tl + 1)));
-                t += 2;
-            }
-            else {
-                f16x8 A0[KS];
-#pragma unroll
-                for (int k = 0; k < KS; ++k)
-                    A0[k] = *reinterpret_cast<const f16x8*>(base + lt * kTileA + k * 1024 + lane * 16);
-                f32x4 acc[NF];
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-                    acc[cb] = XX[cb];
-#pragma unroll
-                for (int k = 0; k < KS; ++k)
-#pragma unroll
-                    for (int cb = 0; cb < NF; ++cb)
-                        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[k], B[cb][k], acc[cb], 0, 0, 0);
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        best[cb][r] = fminf(best[cb][r], key(acc[cb][r], tl));
-                t += 1;
-            }
-            // mixture(s) ending here (further ones without tiles end at the same point)
-            while (t == tEnd && m < m1) {
-                emitMixtureSplit<NF>(a, scores, bestOut, best, m, frame0, lane, g, tmask, eOut);
-                resetBest();
-                ++m;
-                tBeg = tEnd;
-                tEnd = m < m1 ? mixTileOff[m + 1] : T1;
-            }
+    // mixtures ending at tile tNext (and the empty ones after them)
+    const auto finish = [&](uint32_t tNext) {
+        while (m < m1 && tEnd == tNext) {
+            emitMixtureSplit(a, best, m, frame0, lane, g, kmask, eOut);
+            resetBest();
+            ++m;
+            tBeg = tNext;
+            tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
         }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (s & 1)
-        if (s + 2 < nSeg)
-            issueSeg(s + 2);
+    };
+    finish(T0);
+    uint32_t t = T0;
+    for (; t + 4 <= T1; t += 4) {
+        pairStep(R0, R1, t - tBeg);
+        loadTile(t + 4, R0);
+        loadTile(t + 5, R1);
+        finish(t + 2);
+        pairStep(R2, R3, t + 2 - tBeg);
+        loadTile(t + 6, R2);
+        loadTile(t + 7, R3);
+        finish(t + 4);
+    }
+    if (t < T1) {  // one pair left
+        pairStep(R0, R1, t - tBeg);
+        finish(t + 2);
     }
 }
 
@@ -474,18 +338,9 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
     return hipGetLastError();
 }
 
-#ifndef GMM_SPLIT_LDS
-#define GMM_SPLIT_LDS 0  // tiles staged through LDS (scoreSplitSeg): measured slower, off
-#endif
-
 template <int KS>
 static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
-#if GMM_SPLIT_LDS
-    hipLaunchKernelGGL((dev::scoreSplitSeg<kSplitNF, KS>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff, a.scores,
-                       a.best);
-#else
-    hipLaunchKernelGGL((dev::scoreSplit<kSplitNF, KS>), dim3(grid), dim3(256), 0, s, a);
-#endif
+    hipLaunchKernelGGL((dev::scoreSplit<KS>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
 }
 
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream) {

@@ -410,7 +410,15 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
     double             cst = 0;
 
     // ---- split-f16 layout ----
-    if (wantSplit && !out.foldNorm && splitKSteps(D) <= 8 && T > 0) {
+    // key bits: tile number in the mixture (after padding to an even count) and the 2-bit row slot;
+    // at most 8 dropped mantissa bits (reported score within 2^-16 relative), else the f32 kernel
+    uint32_t splitMaxTiles = 2;
+    for (uint32_t m = 0; m < out.nMixtures; ++m)
+        splitMaxTiles = std::max(splitMaxTiles, (out.tiling.mixTileOffset[m + 1] - out.tiling.mixTileOffset[m] + 1) & ~1u);
+    uint32_t splitTileBits = 1;
+    while ((1u << splitTileBits) < splitMaxTiles)
+        ++splitTileBits;
+    if (wantSplit && !out.foldNorm && splitKSteps(D) <= 8 && T > 0 && splitTileBits + 2 <= 8) {
         std::vector<double> maxAbs(D, 0.0);
         double              maxConst = 0;
         for (uint32_t t = 0; t < T; ++t)
@@ -429,8 +437,40 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
         while (b0 < 15 && maxConst / std::ldexp(1.0, b0) > 32768.0)
             ++b0;
         if (finite && maxConst / std::ldexp(1.0, b0) <= 32768.0) {
-            out.split    = true;
-            out.kSteps16 = splitKSteps(D);
+            out.split        = true;
+            out.kSteps16     = splitKSteps(D);
+            out.splitKeyBits = splitTileBits + 2;
+            // even tile count per mixture (the kernel walks tile pairs): a pad tile repeats row 0 of
+            // the mixture's first tile in every row, an exact tie with a lower density index
+            std::vector<uint32_t> padOf;  // [padded tile] -> padded index of the tile whose row 0 it repeats
+            {
+                const Tiling& tg = out.tiling;
+                Tiling        pt;
+                pt.maxEntriesPerMixture = tg.maxEntriesPerMixture;
+                pt.mixTileOffset.assign(out.nMixtures + 1, 0);
+                for (uint32_t m = 0; m < out.nMixtures; ++m) {
+                    const uint32_t b = tg.mixTileOffset[m], e = tg.mixTileOffset[m + 1];
+                    const uint32_t first = static_cast<uint32_t>(pt.tileCovariance.size());
+                    for (uint32_t t = b; t < e; ++t) {
+                        pt.tileCovariance.push_back(tg.tileCovariance[t]);
+                        padOf.push_back(UINT32_MAX);
+                        for (uint32_t r = 0; r < kTileRows; ++r) {
+                            pt.rowEntry.push_back(tg.rowEntry[static_cast<size_t>(t) * kTileRows + r]);
+                            pt.rowDensityInMixture.push_back(tg.rowDensityInMixture[static_cast<size_t>(t) * kTileRows + r]);
+                        }
+                    }
+                    if ((e - b) & 1u) {
+                        pt.tileCovariance.push_back(tg.tileCovariance[b]);
+                        padOf.push_back(first);
+                        pt.rowEntry.insert(pt.rowEntry.end(), kTileRows, UINT32_MAX);
+                        pt.rowDensityInMixture.insert(pt.rowDensityInMixture.end(), kTileRows, UINT32_MAX);
+                    }
+                    pt.mixTileOffset[m + 1] = static_cast<uint32_t>(pt.tileCovariance.size());
+                }
+                pt.nTiles  = static_cast<uint32_t>(pt.tileCovariance.size());
+                out.tiling = std::move(pt);
+            }
+            const uint32_t TP = out.tiling.nTiles;
             for (uint32_t s = 0; s < kSplitLimbs; ++s)
                 out.limbExp[s] = b0 - 11 * static_cast<int32_t>(s);
             // per-dimension power of two that puts max|m''_d| in [2^7, 2^8): m'' and x'' then sit in
@@ -457,14 +497,16 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                 return static_cast<double>(h);
             };
             const uint32_t KS16 = out.kSteps16;
-            out.tileH.assign(static_cast<size_t>(T) * KS16 * kLanes * 8, 0);
+            out.tileH.assign(static_cast<size_t>(TP) * KS16 * kLanes * 8, 0);
             std::vector<uint16_t> row(KS16 * 32);
-            for (uint32_t t = 0; t < T; ++t) {
+            for (uint32_t t = 0; t < TP; ++t) {
                 for (uint32_t r = 0; r < kTileRows; ++r) {
                     std::fill(row.begin(), row.end(), 0);
-                    // a padding row repeats row 0 of its tile (every tile starts with a real row):
-                    // an exact tie with a lower density index never wins, and no +inf/NaN keys
-                    if (rowValues(t, r, m2.data(), cst) || rowValues(t, 0, m2.data(), cst)) {
+                    // a padding row repeats row 0 of its tile (every tile but a pad tile starts with a
+                    // real row; a pad tile repeats row 0 of its mixture's first tile): an exact tie with
+                    // a lower density index never wins, and no +inf/NaN keys
+                    const uint32_t t0 = padOf[t] == UINT32_MAX ? t : padOf[t];
+                    if (rowValues(t, r, m2.data(), cst) || rowValues(t0, 0, m2.data(), cst)) {
                         for (uint32_t k = 0; k < D; ++k) {
                             const float    v  = static_cast<float>(m2[k] * inv[k]);  // exact: power of two
                             const uint16_t hi = h16(v);
@@ -479,6 +521,8 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                             row[3 * D + s]   = l;
                             rem -= std::ldexp(f16v(l), out.limbExp[s]);
                         }
+                        for (uint32_t s = 0; s < kSplitXXLimbs; ++s)
+                            row[3 * D + kSplitLimbs + s] = h16(std::ldexp(1.0, kSplitXXExp[s]));
                     }
                     // fragment order of v_mfma_f32_16x16x32_f16: lane = 16*((k>>3)&3) + row, step k>>5
                     for (uint32_t k = 0; k < KS16 * 32; ++k) {

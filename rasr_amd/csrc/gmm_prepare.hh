@@ -97,6 +97,9 @@ struct PreparedFloat {
     std::vector<uint16_t> tileH;           // [nTiles][kSteps16][64 lanes][8] f16 bits
     std::vector<float>    dimScale;        // [dimension]: 2^a_d, x'' = x' * 2^a_d, m'' = -2 m' / 2^a_d
     int32_t               limbExp[4] = {0, 0, 0, 0};  // b_s: the frame side of limb s is 2^(b_s - e_frame)
+    // split kernel keys: the low splitKeyBits mantissa bits hold (tile in mixture << 2 | row slot);
+    // every mixture has an even number of tiles (pad tiles repeat the mixture's first row)
+    uint32_t              splitKeyBits = 0;
 };
 
 
@@ -108,7 +111,7 @@ struct ShardRange {
 std::string validate(const gmm_mixture_set& ms);
 std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out);
 // wantSplit: lay the model out for the split-f16 kernel when it applies (one covariance,
-// 3*dimension+4 <= 256, row constants below 2^30); out.split says whether it did.
+// 3*dimension+7 <= 256, row constants below 2^30); out.split says whether it did.
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
                          ShardRange shard, PreparedFloat& out, bool wantSplit = false);
 
