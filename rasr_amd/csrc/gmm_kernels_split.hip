@@ -36,6 +36,9 @@
 // minimum is a float key whose low tileBits mantissa bits hold the tile number.
 #include "gmm_device.hh"
 
+#ifndef GMM_SPLIT_DIAG
+#define GMM_SPLIT_DIAG 0  // timing diagnostics only (wrong results): 2 = keys without tags, 4 = no emit
+#endif
 #ifndef GMM_SPLIT_MIN_WAVES
 #define GMM_SPLIT_MIN_WAVES 1
 #endif
@@ -143,12 +146,15 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
 // minimum by (value, tile); the lane group g is resolved at the end of the mixture, where keys
 // equal in value and tag prefer the lower group (lower density index).
 // ---------------------------------------------------------------------------
-
 // end of a mixture: the 4 slot keys of each column block -> (score, density) per frame, reduced
 // across the four 16-lane groups by permlane swaps (r0 of a swap always comes from the lower group);
-// lane l stores frame frame0 + l
+// lane l stores frame frame0 + l.  Straight-line code (no branch splits the basic block it is
+// scheduled into): uniform options are arithmetic, the frame bound is the buffer's num_records.
+// ---------------------------------------------------------------------------
+template <bool BEST>
 __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][4], uint32_t m,
-                                                 uint32_t frame0, int lane, uint32_t g, uint32_t kmask, int eOut) {
+                                                 uint32_t frame0, int lane, uint32_t g, uint32_t kmask, int eOut,
+                                                 float noneScore, float halfScale) {
     uint32_t k[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
@@ -157,10 +163,10 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
     uint32_t w[2], wg[2];
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-        const auto     r    = __builtin_amdgcn_permlane32_swap(k[p], k[p + 2], false, false);
-        const bool     take = r[1] < r[0];
-        w[p]                = take ? r[1] : r[0];
-        wg[p]               = (g & 1u) | (take ? 2u : 0u);
+        const auto r    = __builtin_amdgcn_permlane32_swap(k[p], k[p + 2], false, false);
+        const bool take = r[1] < r[0];
+        w[p]            = take ? r[1] : r[0];
+        wg[p]           = (g & 1u) | (take ? 2u : 0u);
     }
     // groups {even, odd} rows: lane l keeps block l >> 4
     const auto     rk   = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
@@ -169,40 +175,39 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
     const uint32_t key  = take ? rk[1] : rk[0];
     const uint32_t grp  = take ? rg[1] : rg[0];
 
-    const uint32_t f = frame0 + static_cast<uint32_t>(lane);
     // midpoint of the masked bits: within 2^-(24 - keyBits) of the minimum's value
-    const float kv = __uint_as_float((key & ~kmask) | ((kmask + 1u) >> 1));
-    float       score;
-    uint32_t    idx;
-    if (!(kv < 1e37f)) {  // no finite candidate (empty mixture, non-finite frame): Core::Type<Score>::max
-        idx   = 0xffffffffu;
-        score = a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f;
-    }
-    else {
-        idx                = (((key & kmask) >> 2) << 4) | (grp << 2) | (key & 3u);
-        const float scaled = ldexpf(kv, eOut);
-        const float total  = a.offsetK0 != 0.0f ? __fsub_rn(scaled, a.offsetK0) : scaled;
-        score              = a.flavor == 2 ? 0.5f * total : (total < 3.40282347e+38f ? 0.5f * total : total);
-    }
-    if (a.outScale != 1.0f)
-        score = __fmul_rn(a.outScale, score);
-    const size_t o = static_cast<size_t>(m - a.mixBase) * a.scoreStride + f;
-    if (f < a.nFrames) {
-        a.scores[o] = score;
-        if (a.best)
-            a.best[o] = idx;
+    const float kv    = __uint_as_float((key & ~kmask) | ((kmask + 1u) >> 1));
+    const bool  none  = !(kv < 1e37f);  // no finite candidate (empty mixture, non-finite frame)
+    const float total = __fsub_rn(ldexpf(kv, eOut), a.offsetK0);
+    // diagonal-maximum: 0.5 total; batch-float keeps an overflowed total (BatchFeatureScorer.cc:468)
+    const float score = none ? noneScore
+                             : __fmul_rn(a.outScale, (a.flavor == 3 && !(total < 3.40282347e+38f)) ? total : 0.5f * total);
+    const uint32_t idx = none ? 0xffffffffu : ((((key & kmask) >> 2) << 4) | (grp << 2) | (key & 3u));
+    (void)halfScale;
+    const uint32_t mo  = m - a.mixBase;
+    const uint32_t off = static_cast<uint32_t>(frame0 + lane) * 4u;
+    // frames >= nFrames fall outside num_records: the buffer store drops them
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                     static_cast<int>(a.nFrames * 4u), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, off, 0, 0);
+    if constexpr (BEST) {
+        const auto rb = __builtin_amdgcn_make_buffer_rsrc(a.best + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                         static_cast<int>(a.nFrames * 4u), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, 0);
     }
 }
 
 // ---------------------------------------------------------------------------
 // scorer.  A workgroup = 4 waves x 64 frames (4 column blocks of 16) walks a chunk of mixtures on one
 // XCD.  Every mixture has an even number of tiles (host), so the chunk is a flat sequence of tile
-// pairs; the loop body takes two pairs, whose operands live in two named register sets (R0,R1 and
-// R2,R3) loaded two pairs ahead.  Mixture bounds are scalar loads (mixTileOff is a restrict kernel
-// argument): a vector load there would come with an s_waitcnt vmcnt(0) draining the prefetch and the
-// previous mixture's stores.
+// pairs.  Operands of consecutive pairs alternate between two register sets (R0,R1 / R2,R3) loaded
+// two pairs ahead, and the pipeline is software-staged: step p issues the 32 MFMAs of pair p beside
+// the epilogue (tag + min) of pair p-1, interleaved MFMA : VALU by sched_group_barrier, then emits the
+// mixture that pair p-1 ended, if any.  Mixture bounds are scalar
+// loads (mixTileOff is a restrict kernel argument): a vector load there would come with an
+// s_waitcnt vmcnt(0) draining the prefetch.
 // ---------------------------------------------------------------------------
-template <int KS>
+template <int KS, bool BEST>
 __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
                                                                       const uint32_t* __restrict__ mixTileOff) {
     constexpr int  NF   = 4;
@@ -223,6 +228,7 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs
         for (int s = 0; s < KS; ++s)
             A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
     };
+
     const f16x8* fh = static_cast<const f16x8*>(a.frameH);
     f16x8        B[NF][KS];
 #pragma unroll
@@ -253,6 +259,8 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs
     // SGPR (gfx950 VOP3 reads at most one SGPR)
     uint32_t vmask = ~kmask;
     asm volatile("" : "+v"(vmask));
+    // score of a mixture without a finite candidate: Core::Type<Score>::max, halved by diagonal-maximum
+    const float noneScore = __fmul_rn(a.outScale, a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f);
 
     uint32_t   best[NF][4];
     const auto resetBest = [&]() {
@@ -272,57 +280,107 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs
             for (int cb = 0; cb < NF; ++cb)
                 acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
     };
-    // one pair of tiles (tile numbers tl, tl + 1 in the mixture)
-    const auto pairStep = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], uint32_t tl) {
-        f32x4 accA[NF], accB[NF];
-        chain(A0, accA);
-        chain(A1, accB);
+    // epilogue of one pair of tiles (tile numbers tl, tl + 1 in the mixture)
+    const auto pairEpilogue = [&](const f32x4(&acc)[2][NF], uint32_t tl) {
         // per-slot tags as opaque SGPRs: with a visible constant the compiler splits the tag OR off the
-        // v_and_or_b32 into a v_and + v_or3 pair
+        // v_and_or_b32 into a v_and + v_or3 pair (non-volatile asm: no scheduling barrier)
         uint32_t tagA[4], tagB[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             tagA[r] = (tl << 2) | r;
             tagB[r] = ((tl + 1u) << 2) | r;
-            asm volatile("" : "+s"(tagA[r]), "+s"(tagB[r]));
+            asm("" : "+s"(tagA[r]), "+s"(tagB[r]));
         }
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const uint32_t ka = (__float_as_uint(accA[cb][r]) & vmask) | tagA[r];
-                const uint32_t kb = (__float_as_uint(accB[cb][r]) & vmask) | tagB[r];
+                const uint32_t ka = (GMM_SPLIT_DIAG & 2) ? __float_as_uint(acc[0][cb][r])
+                                                         : (__float_as_uint(acc[0][cb][r]) & vmask) | tagA[r];
+                const uint32_t kb = (GMM_SPLIT_DIAG & 2) ? __float_as_uint(acc[1][cb][r])
+                                                         : (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
                 best[cb][r]       = umin3(best[cb][r], ka, kb);
             }
     };
 
     uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
-    // mixtures ending at tile tNext (and the empty ones after them)
-    const auto finish = [&](uint32_t tNext) {
+    const auto emit = [&]() {
+        if (!(GMM_SPLIT_DIAG & 4) || m + 1 == m1)
+            emitMixtureSplit<BEST>(a, best, m, frame0, lane, g, kmask, eOut, noneScore, 0.5f);
+    };
+    // after an emit at tile tNext: next mixture, and the empty ones that also end there (rare path)
+    const auto advance = [&](uint32_t tNext) {
+        ++m;
+        tBeg = tNext;
+        tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
         while (m < m1 && tEnd == tNext) {
-            emitMixtureSplit(a, best, m, frame0, lane, g, kmask, eOut);
-            resetBest();
+            emit();
             ++m;
-            tBeg = tNext;
             tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
         }
     };
-    finish(T0);
-    uint32_t t = T0;
-    for (; t + 4 <= T1; t += 4) {
-        pairStep(R0, R1, t - tBeg);
+    // one pipeline step: the MFMAs of the pair in (A0, A1) into cur beside the epilogue of the pair in
+    // prev, interleaved 1 MFMA : 2 VALU (the operand loads for two pairs ahead follow, then finish())
+    const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
+                          const f32x4(&prev)[2][NF], uint32_t tPrev) {
+        chain(A0, cur[0]);
+        chain(A1, cur[1]);
+        pairEpilogue(prev, tPrev - tBeg);
+#pragma unroll
+        for (int i = 0; i < 24; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    };
+    // the emit of the mixture that ended at tile tNext, if any (a separate block: with the emit inside
+    // the interleaved one, the duplicated step needs more than 256 VGPRs)
+    const auto finish = [&](uint32_t tNext) {
+        if (tNext == tEnd) {
+            emit();
+            resetBest();
+            advance(tNext);
+        }
+    };
+    // the last pair's epilogue (nothing left to overlap it with)
+    const auto drain = [&](const f32x4(&prev)[2][NF], uint32_t tPrev) {
+        pairEpilogue(prev, tPrev - tBeg);
+        finish(tPrev + 2);
+    };
+
+    // mixtures without tiles at the start of the chunk
+    while (m < m1 && tEnd == T0) {
+        emit();
+        ++m;
+        tEnd = m < m1 ? mixTileOff[m + 1] : T0;
+    }
+    if (T0 < T1) {
+        f32x4    accX[2][NF], accY[2][NF];
+        uint32_t t = T0;
+        chain(R0, accX[0]);  // pair 0: nothing to finish beside it
+        chain(R1, accX[1]);
         loadTile(t + 4, R0);
         loadTile(t + 5, R1);
-        finish(t + 2);
-        pairStep(R2, R3, t + 2 - tBeg);
-        loadTile(t + 6, R2);
-        loadTile(t + 7, R3);
-        finish(t + 4);
-    }
-    if (t < T1) {  // one pair left
-        pairStep(R0, R1, t - tBeg);
-        finish(t + 2);
+        t += 2;
+        for (; t + 4 <= T1; t += 4) {
+            step(R2, R3, accY, accX, t - 2);
+            loadTile(t + 4, R2);
+            loadTile(t + 5, R3);
+            finish(t);
+            step(R0, R1, accX, accY, t);
+            loadTile(t + 6, R0);
+            loadTile(t + 7, R1);
+            finish(t + 2);
+        }
+        if (t < T1) {  // one more pair (in R2, R3)
+            step(R2, R3, accY, accX, t - 2);
+            finish(t);
+            drain(accY, t);
+        }
+        else {
+            drain(accX, t - 2);
+        }
     }
 }
 
@@ -340,7 +398,10 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
 
 template <int KS>
 static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL((dev::scoreSplit<KS>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+    if (a.best)
+        hipLaunchKernelGGL((dev::scoreSplit<KS, true>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+    else
+        hipLaunchKernelGGL((dev::scoreSplit<KS, false>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
 }
 
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream) {
