@@ -161,12 +161,15 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
                   - ms.mixture_offsets[scorer.shards[rank][0]]) if sharded else int(ms.n_entries)
     algo = 2.0 * args.dim * d_local * frames_per_gpu  # one multiply-add per (frame, density, component)
     kernel = sc.main_kernel()
-    if kernel == "scoreSplit":
+    split = kernel in ("scoreSplit", "scoreSplit32")
+    if split:
         # f32-accurate contraction on the f16 matrix cores: 3 f16 products per f32 multiply-add, so the
         # roofline for this arithmetic is the dense f16 peak / 3; the MFMA work actually issued covers
-        # K = 32 * ceil((3 D + 4) / 32) per (frame, density) (row constant limbs + padding)
+        # K = 3 D + 7 (row-constant and ||x'||^2 limbs) padded to the K step (32 for 16x16x32, 16 for
+        # 32x32x16) per (frame, density)
         peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PRODUCTS
-        k_issued = 32 * ((3 * args.dim + 4 + 31) // 32)
+        kq = 16 if kernel == "scoreSplit32" else 32
+        k_issued = kq * ((3 * args.dim + 7 + kq - 1) // kq)
         issued = 2.0 * k_issued * d_local * frames_per_gpu
     elif mode == "fp32":
         peak = PEAK_F32_MFMA_TFLOPS
@@ -179,7 +182,7 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
     res = {
         "value": total_frames / dt_max,
         "ms_per_step": dt_max / args.steps * 1e3,
-        "dtype": dtype if kernel != "scoreSplit" else
+        "dtype": dtype if not split else
         "f32 (operands split into 2 f16 pieces, 3 f16 MFMA products, f32 accumulate)",
         "frames_per_gpu": frames_per_gpu,
         "roofline": {
@@ -195,7 +198,7 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
             "issued_mfma_flop_per_launch": issued,
             "issued_mfma_tflops": issued / sec / 1e12,
             "issued_mfma_frac_of_dtype_peak": issued / sec / 1e12 / (
-                PEAK_F16_MFMA_TFLOPS if kernel == "scoreSplit" else peak),
+                PEAK_F16_MFMA_TFLOPS if split else peak),
             "output_bytes_per_launch": m_local * frames_per_gpu * (4 + (0 if best is None else 4)),
         },
     }

@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get("RASR_GMM_LIB") or os.path.join(_HERE, "lib", "librasr
 
 GMM_OK = 0
 GMM_FLAG_NATIVE_F32 = 1  # gmm_scorer_config.flags
+GMM_FLAG_SPLIT_TILE16 = 2
+GMM_FLAG_SPLIT_TILE32 = 4
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0

@@ -77,7 +77,8 @@ struct gmm_scorer {
     bool              multiCov   = false;
     bool              foldNorm   = false;
     bool              split      = false;  // float types on the split-f16 kernel
-    uint32_t          kSteps16   = 0;
+    uint32_t          kSteps16   = 0;      // split kernel: K steps (32 wide for 16-row tiles, 16 wide for 32-row)
+    uint32_t          splitRows  = 16;     // split kernel tile height
     uint32_t          tileBits   = 1;
     float             offsetK0   = 0;
     // quantized scalars
@@ -239,7 +240,7 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         GMM_HIP_CHECK(span.end());
     }
     else if (s->split) {
-        GMM_HIP_CHECK(launchPrepareFramesSplit(frames, nFrames, frameStride, nPadCall, s->D, s->kSteps16, s->dIsv,
+        GMM_HIP_CHECK(launchPrepareFramesSplit(frames, nFrames, frameStride, nPadCall, s->D, s->splitRows, s->kSteps16, s->dIsv,
                                                s->dDimScale, s->dLimbExp, s->dFrameH, s->dFrameXX, s->dFrameExp,
                                                stream));
         SplitArgs a{};
@@ -263,7 +264,7 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.outScale    = s->cfg.score_scale;
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
-        GMM_HIP_CHECK(launchScoreSplit(a, s->kSteps16, stream));
+        GMM_HIP_CHECK(launchScoreSplit(a, s->splitRows, s->kSteps16, stream));
         GMM_HIP_CHECK(span.end());
     }
     else {
@@ -397,11 +398,14 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     else {
         PreparedFloat p;
         std::string   err = prepareFloat(*ms, flavor, cfg.mixture_weight_scale, cfg.gaussian_scale, shard, p,
-                                         (cfg.flags & GMM_FLAG_NATIVE_F32) == 0);
+                                         (cfg.flags & GMM_FLAG_NATIVE_F32) == 0,
+                                         (cfg.flags & GMM_FLAG_SPLIT_TILE16) ? 16u
+                                                                              : ((cfg.flags & GMM_FLAG_SPLIT_TILE32) ? 32u : 0u));
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
         s->split    = p.split;
         s->kSteps16 = p.kSteps16;
+        s->splitRows = p.splitRows;
         s->nMix       = p.nMixtures;
         s->kSteps     = p.kSteps;
         s->multiCov   = s->C > 1;
@@ -412,7 +416,7 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         s->mixTileOff = p.tiling.mixTileOffset;
         if (s->split) {
             const std::vector<int32_t> limbs(p.limbExp, p.limbExp + kSplitLimbs);
-            const size_t               nH = static_cast<size_t>(s->nFramesPad) * p.kSteps16 * 32;
+            const size_t nH = static_cast<size_t>(s->nFramesPad) * p.kSteps16 * (p.splitRows == 32 ? 16 : 32);
             if ((rc = upload(reinterpret_cast<uint16_t**>(&s->dTileA), p.tileH, kTilePad * kLanes * 8 * p.kSteps16)) ||
                 (rc = upload(&s->dDimScale, p.dimScale)) || (rc = upload(&s->dLimbExp, limbs)) ||
                 (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)))
@@ -569,7 +573,7 @@ int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLau
     if (nLaunches)
         *nLaunches = 2;
     if (name)
-        *name = s->quantized ? "scoreI8" : (s->split ? "scoreSplit" : "scoreF32");
+        *name = s->quantized ? "scoreI8" : (s->split ? (s->splitRows == 32 ? "scoreSplit32" : "scoreSplit") : "scoreF32");
     return GMM_OK;
 }
 

@@ -68,8 +68,11 @@ constexpr uint32_t kSplitXXLimbs = 3;
 constexpr int kSplitXXExp[kSplitXXLimbs] = {15, 4, -7};
 // K layout of the split kernel: [0,D) mh*xh, [D,2D) mh*xl, [2D,3D) ml*xh, [3D,3D+4) row-constant
 // limbs, [3D+4,3D+7) ||x'||^2 limbs
-inline uint32_t splitKSteps(uint32_t dimension) {
+inline uint32_t splitKSteps(uint32_t dimension) {  // K/32 steps of v_mfma_f32_16x16x32_f16
     return (3 * dimension + kSplitLimbs + kSplitXXLimbs + 31) / 32;
+}
+inline uint32_t splitKSteps32(uint32_t dimension) {  // K/16 steps of v_mfma_f32_32x32x16_f16
+    return (3 * dimension + kSplitLimbs + kSplitXXLimbs + 15) / 16;
 }
 
 struct SplitArgs {
@@ -96,10 +99,11 @@ hipError_t launchPrepareFramesF32(const float* frames, uint32_t nFrames, uint32_
                                   uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, int foldNorm, const float* isv, float* frameX,
                                   float* frameXX, hipStream_t stream);
 hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
-                                    uint32_t D, uint32_t KS16, const float* isv, const float* dimScale,
+                                    uint32_t D, uint32_t rows, uint32_t kSteps, const float* isv, const float* dimScale,
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream);
-hipError_t launchScoreSplit(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream);
+hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps, hipStream_t stream);
+constexpr uint32_t kSplit32MaxKSteps = 10;  // 32-row split kernel instantiated for K/16 <= 10 (D <= 51)
 hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 hipError_t launchScoreF32(const F32Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 

@@ -63,6 +63,7 @@ __device__ __forceinline__ uint16_t h16bits(float v) {
 //   frameH  [nFramesPad/16][KS16][64][8] f16 (B fragments), frameXX = ||x'||^2 * 2^-e,
 //   frameExp = e.  Rows >= nFrames are zero.
 // ---------------------------------------------------------------------------
+template <int ROWS>
 __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restrict__ frames, uint32_t nFrames,
                                                            uint32_t frameStride, uint32_t nFramesRead, uint32_t D,
                                                            uint32_t KS16, const float* __restrict__ isv,
@@ -110,8 +111,10 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
             rem            = __fsub_rn(rem, lv);
         }
     }
-    const uint32_t fb = f >> 4, col = f & 15;
-    for (uint32_t q = 0; q < KS16 * 4; ++q) {  // groups of 8 consecutive k
+    // B fragments: 16 rows: frame block f/16, lane 16*((k>>3)&3) + f%16, step k>>5;
+    //              32 rows: frame block f/32, lane 32*((k>>3)&1) + f%32, step k>>4
+    const uint32_t fb = f / ROWS, col = f % ROWS;
+    for (uint32_t q = 0; q < KS16 * (ROWS == 32 ? 2 : 4); ++q) {  // groups of 8 consecutive k
         uint32_t w[4] = {0, 0, 0, 0};
         if (valid)
             for (uint32_t j = 0; j < 8; ++j) {
@@ -133,8 +136,9 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
                 }
                 w[j >> 1] |= static_cast<uint32_t>(h) << (16 * (j & 1));
             }
-        // step q>>2, lane group q&3
-        frameH[(static_cast<size_t>(fb) * KS16 + (q >> 2)) * 64 + 16 * (q & 3) + col] = u32x4{w[0], w[1], w[2], w[3]};
+        const uint32_t step = ROWS == 32 ? q >> 1 : q >> 2;
+        const uint32_t ln   = ROWS == 32 ? 32 * (q & 1) + col : 16 * (q & 3) + col;
+        frameH[(static_cast<size_t>(fb) * KS16 + step) * 64 + ln] = u32x4{w[0], w[1], w[2], w[3]};
     }
 }
 
@@ -384,15 +388,209 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs
     }
 }
 
+// ---------------------------------------------------------------------------
+// 32-density tiles on v_mfma_f32_32x32x16_f16 (mixtures of <= 512 densities).  Per 16x16x32-equivalent
+// of work the 32x32x16 MFMA holds the SIMD's vector issue half as long (8 of 32 cycles), which leaves
+// the issue slots to the epilogue VALU.  Lane l (r = l & 31, h = l >> 5) holds A[row r][k = 16s+8h+j],
+// B[k = 16s+8h+j][frame r] and accumulator register i = row (i & 3) + 8 (i >> 2) + 4 h of frame r.
+// A wave owns 64 frames (two 32-frame blocks); one pipeline step = one tile = 2 x KS MFMAs beside
+// the epilogue of the previous tile.  Keys: value bits with the low keyBits replaced by
+// (tile << 4 | i); four slots per block keep the minimum over registers {q, q+4, q+8, q+12}.
+// ---------------------------------------------------------------------------
+template <bool BEST>
+__device__ __forceinline__ void emitMixtureSplit32(const SplitArgs& a, const uint32_t (&best)[2][4], uint32_t m,
+                                                   uint32_t frame0, int lane, uint32_t kmask, int eOut,
+                                                   float noneScore) {
+    uint32_t k[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+        k[b] = min(umin3(best[b][0], best[b][1], best[b][2]), best[b][3]);
+    // lanes < 32 keep block 0, lanes >= 32 block 1; r[0] from lane half h = 0, r[1] from h = 1
+    const auto     r    = __builtin_amdgcn_permlane32_swap(k[0], k[1], false, false);
+    // (value, tile) first, then the row in the tile: row(i, h) = (i & 3) + 8 (i >> 2) + 4 h
+    const uint32_t hi0  = r[0] & ~15u, hi1 = r[1] & ~15u;
+    const uint32_t row0 = (r[0] & 3u) | ((r[0] & 12u) << 1), row1 = ((r[1] & 3u) | ((r[1] & 12u) << 1)) + 4u;
+    const bool     take = hi1 < hi0 || (hi1 == hi0 && row1 < row0);
+    const uint32_t key  = take ? r[1] : r[0];
+    const uint32_t row  = take ? row1 : row0;
+
+    const float kv    = __uint_as_float((key & ~kmask) | ((kmask + 1u) >> 1));
+    const bool  none  = !(kv < 1e37f);
+    const float total = __fsub_rn(ldexpf(kv, eOut), a.offsetK0);
+    const float score = none ? noneScore
+                             : __fmul_rn(a.outScale, (a.flavor == 3 && !(total < 3.40282347e+38f)) ? total : 0.5f * total);
+    const uint32_t idx = none ? 0xffffffffu : ((((key & kmask) >> 4) << 5) | row);
+    const uint32_t mo  = m - a.mixBase;
+    const uint32_t off = static_cast<uint32_t>(frame0 + lane) * 4u;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                     static_cast<int>(a.nFrames * 4u), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, off, 0, 0);
+    if constexpr (BEST) {
+        const auto rb = __builtin_amdgcn_make_buffer_rsrc(a.best + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                         static_cast<int>(a.nFrames * 4u), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, 0);
+    }
+}
+
+template <int KS, bool BEST>
+__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit32(SplitArgs a,
+                                                                        const uint32_t* __restrict__ mixTileOff) {
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    const int      lane = threadIdx.x & 63;
+    const int      wave = threadIdx.x >> 6;
+    uint32_t       chunk, ft;
+    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
+        return;
+    const uint32_t frame0 = ft * 256u + static_cast<uint32_t>(wave) * 64u;
+    const uint32_t fb0    = frame0 / 32u;
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
+
+    const f16x8* th       = static_cast<const f16x8*>(a.tileH);
+    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS]) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+    };
+    const f16x8* fh = static_cast<const f16x8*>(a.frameH);
+    f16x8        B[2][KS];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            B[b][s] = fh[(static_cast<size_t>(fb0 + b) * KS + s) * 64 + lane];
+    const int eOut = a.frameExp[frame0 + lane];
+    // frame operands complete before the tile prefetch (see scoreSplit)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            asm volatile("" ::"v"(B[b][s]));
+    asm volatile("" ::"v"(eOut));
+
+    f16x8 R0[KS], R1[KS];  // tiles t (even steps) and t + 1; padded tile array: loads past T1 stay in bounds
+    loadTile(T0, R0);
+    loadTile(T0 + 1, R1);
+
+    const uint32_t kmask = (1u << a.tileBits) - 1u;
+    uint32_t       vmask = ~kmask;
+    asm volatile("" : "+v"(vmask));
+    const float noneScore = __fmul_rn(a.outScale, a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f);
+
+    uint32_t   best[2][4];
+    const auto resetBest = [&]() {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                best[b][q] = 0xffffffffu;
+    };
+    const auto chain = [&](const f16x8(&A)[KS], f32x16(&acc)[2]) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+            acc[b] = f32x16{};  // ||x'||^2 is in K: the chain starts from an inline 0
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[b][s], acc[b], 0, 0, 0);
+    };
+    const auto epilogue = [&](const f32x16(&acc)[2], uint32_t tl) {
+        uint32_t tag[16];  // opaque SGPRs (one v_and_or_b32 per value)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            tag[i] = (tl << 4) | static_cast<uint32_t>(i);
+            asm("" : "+s"(tag[i]));
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t k0 = (__float_as_uint(acc[b][q]) & vmask) | tag[q];
+                const uint32_t k1 = (__float_as_uint(acc[b][q + 4]) & vmask) | tag[q + 4];
+                const uint32_t k2 = (__float_as_uint(acc[b][q + 8]) & vmask) | tag[q + 8];
+                const uint32_t k3 = (__float_as_uint(acc[b][q + 12]) & vmask) | tag[q + 12];
+                best[b][q]        = umin3(umin3(best[b][q], k0, k1), k2, k3);
+            }
+    };
+
+    uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
+    resetBest();
+    const auto emit    = [&]() { emitMixtureSplit32<BEST>(a, best, m, frame0, lane, kmask, eOut, noneScore); };
+    const auto advance = [&](uint32_t tNext) {
+        ++m;
+        tBeg = tNext;
+        tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        while (m < m1 && tEnd == tNext) {
+            emit();
+            ++m;
+            tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        }
+    };
+    const auto finish = [&](uint32_t tNext) {
+        if (tNext == tEnd) {
+            emit();
+            resetBest();
+            advance(tNext);
+        }
+    };
+    // MFMAs of the tile in A into cur beside the epilogue of tile tPrev (in prev), 1 MFMA : 3 VALU
+    const auto step = [&](const f16x8(&A)[KS], f32x16(&cur)[2], const f32x16(&prev)[2], uint32_t tPrev) {
+        chain(A, cur);
+        epilogue(prev, tPrev - tBeg);
+#pragma unroll
+        for (int i = 0; i < 2 * KS; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+        }
+    };
+
+    while (m < m1 && tEnd == T0) {  // mixtures without tiles at the start of the chunk
+        emit();
+        ++m;
+        tEnd = m < m1 ? mixTileOff[m + 1] : T0;
+    }
+    if (T0 < T1) {
+        f32x16   accX[2], accY[2];
+        uint32_t t = T0;
+        chain(R0, accX);  // tile T0: nothing to finish beside it
+        loadTile(t + 2, R0);
+        t += 1;
+        for (; t + 2 <= T1; t += 2) {
+            step(R1, accY, accX, t - 1);
+            loadTile(t + 2, R1);
+            finish(t);
+            step(R0, accX, accY, t);
+            loadTile(t + 3, R0);
+            finish(t + 1);
+        }
+        if (t < T1) {  // one more tile (in R1)
+            step(R1, accY, accX, t - 1);
+            finish(t);
+            epilogue(accY, t - tBeg);
+            finish(t + 1);
+        }
+        else {
+            epilogue(accX, t - 1 - tBeg);
+            finish(t);
+        }
+    }
+}
+
 }  // namespace dev
 
 hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
-                                    uint32_t D, uint32_t KS16, const float* isv, const float* dimScale,
+                                    uint32_t D, uint32_t rows, uint32_t kSteps, const float* isv, const float* dimScale,
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream) {
-    hipLaunchKernelGGL(dev::prepareFramesSplit, dim3((nFramesRead + 255) / 256), dim3(256), 0, stream, frames, nFrames,
-                       frameStride, nFramesRead, D, KS16, isv, dimScale, limbExp,
-                       static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
+    if (rows == 32)
+        hipLaunchKernelGGL(dev::prepareFramesSplit<32>, dim3((nFramesRead + 255) / 256), dim3(256), 0, stream, frames,
+                           nFrames, frameStride, nFramesRead, D, kSteps, isv, dimScale, limbExp,
+                           static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
+    else
+        hipLaunchKernelGGL(dev::prepareFramesSplit<16>, dim3((nFramesRead + 255) / 256), dim3(256), 0, stream, frames,
+                           nFrames, frameStride, nFramesRead, D, kSteps, isv, dimScale, limbExp,
+                           static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
     return hipGetLastError();
 }
 
@@ -404,10 +602,34 @@ static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
         hipLaunchKernelGGL((dev::scoreSplit<KS, false>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
 }
 
-hipError_t launchScoreSplit(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream) {
+template <int KS>
+static void launchSplit32K(const SplitArgs& a, uint32_t grid, hipStream_t s) {
+    if (a.best)
+        hipLaunchKernelGGL((dev::scoreSplit32<KS, true>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+    else
+        hipLaunchKernelGGL((dev::scoreSplit32<KS, false>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+}
+
+hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps16, hipStream_t stream) {
     const uint32_t grid = 8u * ((a.nChunks + 7u) / 8u) * a.nFrameTiles;
     if (grid == 0)
         return hipSuccess;
+    if (rows == 32) {
+        switch (kSteps16) {
+            case 1: launchSplit32K<1>(a, grid, stream); break;
+            case 2: launchSplit32K<2>(a, grid, stream); break;
+            case 3: launchSplit32K<3>(a, grid, stream); break;
+            case 4: launchSplit32K<4>(a, grid, stream); break;
+            case 5: launchSplit32K<5>(a, grid, stream); break;
+            case 6: launchSplit32K<6>(a, grid, stream); break;
+            case 7: launchSplit32K<7>(a, grid, stream); break;
+            case 8: launchSplit32K<8>(a, grid, stream); break;
+            case 9: launchSplit32K<9>(a, grid, stream); break;
+            case 10: launchSplit32K<10>(a, grid, stream); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (kSteps16) {
         case 1: launchSplitK<1>(a, grid, stream); break;
         case 2: launchSplitK<2>(a, grid, stream); break;

@@ -118,13 +118,14 @@ std::string validate(const gmm_mixture_set& ms) {
     return "";
 }
 
-static void buildTiling(const gmm_mixture_set& ms, ShardRange shard, Tiling& t) {
+static void buildTiling(const gmm_mixture_set& ms, ShardRange shard, Tiling& t, uint32_t rows = kTileRows) {
     const uint32_t nMix = shard.end - shard.begin;
     t.mixTileOffset.assign(nMix + 1, 0);
     t.tileCovariance.clear();
     t.rowEntry.clear();
     t.rowDensityInMixture.clear();
     t.maxEntriesPerMixture = 0;
+    t.rows                 = rows;
     std::vector<uint32_t> order;
     for (uint32_t mi = 0; mi < nMix; ++mi) {
         const uint32_t m = shard.begin + mi;
@@ -142,9 +143,9 @@ static void buildTiling(const gmm_mixture_set& ms, ShardRange shard, Tiling& t) 
             size_t         j   = i;
             while (j < order.size() && ms.density_covariance[ms.mixture_densities[order[j]]] == cov)
                 ++j;
-            for (size_t r0 = i; r0 < j; r0 += kTileRows) {
+            for (size_t r0 = i; r0 < j; r0 += rows) {
                 t.tileCovariance.push_back(cov);
-                for (uint32_t r = 0; r < kTileRows; ++r) {
+                for (uint32_t r = 0; r < rows; ++r) {
                     if (r0 + r < j) {
                         t.rowEntry.push_back(order[r0 + r]);
                         t.rowDensityInMixture.push_back(order[r0 + r] - b);
@@ -315,7 +316,7 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
 // ---------------------------------------------------------------------------
 
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
-                         ShardRange shard, PreparedFloat& out, bool wantSplit) {
+                         ShardRange shard, PreparedFloat& out, bool wantSplit, uint32_t splitRowsWanted) {
     std::string err = validate(ms);
     if (!err.empty())
         return err;
@@ -387,10 +388,9 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
             return "float scorer supports at most 4096 densities per mixture";  // key precision 2^-15
     }
 
-    // one row of the contraction: m2[k] = -2 m'_k (f32, as the native kernel's operand) and the
-    // row constant ||m'||^2 + c_d + K0 (f64); false for a padding row
-    const auto rowValues = [&](uint32_t t, uint32_t r, float* m2, double& cst) -> bool {
-        const uint32_t e = out.tiling.rowEntry[static_cast<size_t>(t) * kTileRows + r];
+    // one row of the contraction for entry e: m2[k] = -2 m'_k (f32, as the native kernel's operand)
+    // and the row constant ||m'||^2 + c_d + K0 (f64); false for a padding row (e == UINT32_MAX)
+    const auto entryValues = [&](uint32_t e, float* m2, double& cst) -> bool {
         if (e == UINT32_MAX)
             return false;
         const uint32_t dns  = ms.mixture_densities[e];
@@ -406,28 +406,42 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
         cst = mm + rowConstant(e) + out.offsetK0;
         return true;
     };
+    const auto rowValues = [&](uint32_t t, uint32_t r, float* m2, double& cst) -> bool {
+        return entryValues(out.tiling.rowEntry[static_cast<size_t>(t) * kTileRows + r], m2, cst);
+    };
     std::vector<float> m2(D);
     double             cst = 0;
 
     // ---- split-f16 layout ----
-    // key bits: tile number in the mixture (after padding to an even count) and the 2-bit row slot;
-    // at most 8 dropped mantissa bits (reported score within 2^-16 relative), else the f32 kernel
-    uint32_t splitMaxTiles = 2;
+    // Tile height: 16 rows (v_mfma_f32_16x16x32_f16, tile pairs, keys (tile << 2 | slot)) or 32 rows
+    // (v_mfma_f32_32x32x16_f16, keys (tile << 4 | accumulator register)); keys drop at most 8 mantissa
+    // bits (the reported score within 2^-16 relative), else the f32 kernel.  32 rows by default only
+    // where their 16-wide K steps save a step over the 32-wide ones (e.g. D = 45: K 144 vs 160): the
+    // chip holds a lower clock on the 32x32 shape (D = 39, K 128 both: 1.44 vs 1.38 ms).
+    const auto bitsFor = [](uint32_t n) {
+        uint32_t b = 1;
+        while ((1u << b) < n)
+            ++b;
+        return b;
+    };
+    uint32_t maxEntries = 1;
     for (uint32_t m = 0; m < out.nMixtures; ++m)
-        splitMaxTiles = std::max(splitMaxTiles, (out.tiling.mixTileOffset[m + 1] - out.tiling.mixTileOffset[m] + 1) & ~1u);
-    uint32_t splitTileBits = 1;
-    while ((1u << splitTileBits) < splitMaxTiles)
-        ++splitTileBits;
-    if (wantSplit && !out.foldNorm && splitKSteps(D) <= 8 && T > 0 && splitTileBits + 2 <= 8) {
+        maxEntries = std::max(maxEntries, ms.mixture_offsets[shard.begin + m + 1] - ms.mixture_offsets[shard.begin + m]);
+    const uint32_t keyBits32 = bitsFor((maxEntries + 31) / 32) + 4;
+    const uint32_t keyBits16 = bitsFor(((maxEntries + 15) / 16 + 1) & ~1u) + 2;
+    const bool     fits32    = keyBits32 <= 8 && splitKSteps32(D) <= kSplit32MaxKSteps;
+    const bool     saves32   = splitKSteps32(D) * 16 < splitKSteps(D) * 32;
+    const bool     want32    = splitRowsWanted == 32 || (splitRowsWanted == 0 && saves32);
+    const uint32_t rows      = (fits32 && (want32 || keyBits16 > 8)) ? 32 : (keyBits16 <= 8 ? 16 : 0);
+    if (wantSplit && !out.foldNorm && splitKSteps(D) <= 8 && T > 0 && rows != 0) {
         std::vector<double> maxAbs(D, 0.0);
         double              maxConst = 0;
-        for (uint32_t t = 0; t < T; ++t)
-            for (uint32_t r = 0; r < kTileRows; ++r)
-                if (rowValues(t, r, m2.data(), cst)) {
-                    for (uint32_t k = 0; k < D; ++k)
-                        maxAbs[k] = std::max(maxAbs[k], std::fabs(static_cast<double>(m2[k])));
-                    maxConst = std::max(maxConst, std::fabs(cst));
-                }
+        for (uint32_t e : out.tiling.rowEntry)
+            if (entryValues(e, m2.data(), cst)) {
+                for (uint32_t k = 0; k < D; ++k)
+                    maxAbs[k] = std::max(maxAbs[k], std::fabs(static_cast<double>(m2[k])));
+                maxConst = std::max(maxConst, std::fabs(cst));
+            }
         bool finite = std::isfinite(maxConst);
         for (double v : maxAbs)
             finite = finite && std::isfinite(v);
@@ -438,38 +452,47 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
             ++b0;
         if (finite && maxConst / std::ldexp(1.0, b0) <= 32768.0) {
             out.split        = true;
-            out.kSteps16     = splitKSteps(D);
-            out.splitKeyBits = splitTileBits + 2;
-            // even tile count per mixture (the kernel walks tile pairs): a pad tile repeats row 0 of
-            // the mixture's first tile in every row, an exact tie with a lower density index
-            std::vector<uint32_t> padOf;  // [padded tile] -> padded index of the tile whose row 0 it repeats
-            {
-                const Tiling& tg = out.tiling;
-                Tiling        pt;
-                pt.maxEntriesPerMixture = tg.maxEntriesPerMixture;
+            out.splitRows    = rows;
+            out.kSteps16     = rows == 32 ? splitKSteps32(D) : splitKSteps(D);
+            out.splitKeyBits = rows == 32 ? keyBits32 : keyBits16;
+            // the split tiling; 16-row tiles: an even tile count per mixture (the kernel walks tile
+            // pairs), a pad tile repeating row 0 of the mixture's first tile in every row (an exact tie
+            // with a lower density index never wins)
+            Tiling st;
+            buildTiling(ms, shard, st, rows);
+            std::vector<uint32_t> fillEntry(st.nTiles, UINT32_MAX);  // [tile] entry a padding row repeats
+            for (uint32_t t = 0; t < st.nTiles; ++t)
+                fillEntry[t] = st.rowEntry[static_cast<size_t>(t) * rows];
+            if (rows == 16) {
+                Tiling                pt;
+                std::vector<uint32_t> pf;
+                pt.rows                 = rows;
+                pt.maxEntriesPerMixture = st.maxEntriesPerMixture;
                 pt.mixTileOffset.assign(out.nMixtures + 1, 0);
                 for (uint32_t m = 0; m < out.nMixtures; ++m) {
-                    const uint32_t b = tg.mixTileOffset[m], e = tg.mixTileOffset[m + 1];
-                    const uint32_t first = static_cast<uint32_t>(pt.tileCovariance.size());
+                    const uint32_t b = st.mixTileOffset[m], e = st.mixTileOffset[m + 1];
                     for (uint32_t t = b; t < e; ++t) {
-                        pt.tileCovariance.push_back(tg.tileCovariance[t]);
-                        padOf.push_back(UINT32_MAX);
-                        for (uint32_t r = 0; r < kTileRows; ++r) {
-                            pt.rowEntry.push_back(tg.rowEntry[static_cast<size_t>(t) * kTileRows + r]);
-                            pt.rowDensityInMixture.push_back(tg.rowDensityInMixture[static_cast<size_t>(t) * kTileRows + r]);
-                        }
+                        pt.tileCovariance.push_back(st.tileCovariance[t]);
+                        pf.push_back(fillEntry[t]);
+                        pt.rowEntry.insert(pt.rowEntry.end(), st.rowEntry.begin() + static_cast<size_t>(t) * rows,
+                                           st.rowEntry.begin() + static_cast<size_t>(t + 1) * rows);
+                        pt.rowDensityInMixture.insert(pt.rowDensityInMixture.end(),
+                                                      st.rowDensityInMixture.begin() + static_cast<size_t>(t) * rows,
+                                                      st.rowDensityInMixture.begin() + static_cast<size_t>(t + 1) * rows);
                     }
                     if ((e - b) & 1u) {
-                        pt.tileCovariance.push_back(tg.tileCovariance[b]);
-                        padOf.push_back(first);
-                        pt.rowEntry.insert(pt.rowEntry.end(), kTileRows, UINT32_MAX);
-                        pt.rowDensityInMixture.insert(pt.rowDensityInMixture.end(), kTileRows, UINT32_MAX);
+                        pt.tileCovariance.push_back(st.tileCovariance[b]);
+                        pf.push_back(fillEntry[b]);
+                        pt.rowEntry.insert(pt.rowEntry.end(), rows, UINT32_MAX);
+                        pt.rowDensityInMixture.insert(pt.rowDensityInMixture.end(), rows, UINT32_MAX);
                     }
                     pt.mixTileOffset[m + 1] = static_cast<uint32_t>(pt.tileCovariance.size());
                 }
-                pt.nTiles  = static_cast<uint32_t>(pt.tileCovariance.size());
-                out.tiling = std::move(pt);
+                pt.nTiles = static_cast<uint32_t>(pt.tileCovariance.size());
+                st        = std::move(pt);
+                fillEntry = std::move(pf);
             }
+            out.tiling      = std::move(st);
             const uint32_t TP = out.tiling.nTiles;
             for (uint32_t s = 0; s < kSplitLimbs; ++s)
                 out.limbExp[s] = b0 - 11 * static_cast<int32_t>(s);
@@ -496,17 +519,16 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                 std::memcpy(&h, &b, 2);
                 return static_cast<double>(h);
             };
-            const uint32_t KS16 = out.kSteps16;
-            out.tileH.assign(static_cast<size_t>(TP) * KS16 * kLanes * 8, 0);
-            std::vector<uint16_t> row(KS16 * 32);
+            // K per tile row: kSteps16 steps of 32 (16-row tiles) or of 16 (32-row tiles)
+            const uint32_t KW = out.kSteps16 * (rows == 32 ? 16 : 32);
+            out.tileH.assign(static_cast<size_t>(TP) * rows * KW, 0);
+            std::vector<uint16_t> row(KW);
             for (uint32_t t = 0; t < TP; ++t) {
-                for (uint32_t r = 0; r < kTileRows; ++r) {
+                for (uint32_t r = 0; r < rows; ++r) {
                     std::fill(row.begin(), row.end(), 0);
-                    // a padding row repeats row 0 of its tile (every tile but a pad tile starts with a
-                    // real row; a pad tile repeats row 0 of its mixture's first tile): an exact tie with
-                    // a lower density index never wins, and no +inf/NaN keys
-                    const uint32_t t0 = padOf[t] == UINT32_MAX ? t : padOf[t];
-                    if (rowValues(t, r, m2.data(), cst) || rowValues(t0, 0, m2.data(), cst)) {
+                    // a padding row repeats row 0 of its tile (a pad tile: of its mixture's first tile)
+                    if (entryValues(out.tiling.rowEntry[static_cast<size_t>(t) * rows + r], m2.data(), cst) ||
+                        entryValues(fillEntry[t], m2.data(), cst)) {
                         for (uint32_t k = 0; k < D; ++k) {
                             const float    v  = static_cast<float>(m2[k] * inv[k]);  // exact: power of two
                             const uint16_t hi = h16(v);
@@ -524,10 +546,12 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                         for (uint32_t s = 0; s < kSplitXXLimbs; ++s)
                             row[3 * D + kSplitLimbs + s] = h16(std::ldexp(1.0, kSplitXXExp[s]));
                     }
-                    // fragment order of v_mfma_f32_16x16x32_f16: lane = 16*((k>>3)&3) + row, step k>>5
-                    for (uint32_t k = 0; k < KS16 * 32; ++k) {
-                        const uint32_t lane = 16 * ((k >> 3) & 3) + r;
-                        out.tileH[((static_cast<size_t>(t) * KS16 + (k >> 5)) * kLanes + lane) * 8 + (k & 7)] = row[k];
+                    // fragment order: v_mfma_f32_16x16x32_f16 lane = 16*((k>>3)&3) + row, step k>>5;
+                    // v_mfma_f32_32x32x16_f16 lane = 32*((k>>3)&1) + row, step k>>4
+                    for (uint32_t k = 0; k < KW; ++k) {
+                        const uint32_t lane = rows == 32 ? 32 * ((k >> 3) & 1) + r : 16 * ((k >> 3) & 3) + r;
+                        const uint32_t step = rows == 32 ? k >> 4 : k >> 5;
+                        out.tileH[((static_cast<size_t>(t) * out.kSteps16 + step) * kLanes + lane) * 8 + (k & 7)] = row[k];
                     }
                 }
             }

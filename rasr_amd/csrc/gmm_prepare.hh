@@ -57,7 +57,8 @@ struct Tiling {
     std::vector<uint32_t> mixTileOffset;   // [nMixtures+1] (shard-relative mixtures)
     std::vector<uint32_t> tileCovariance;  // [nTiles]
     std::vector<uint32_t> rowEntry;        // [nTiles*16] entry index or UINT32_MAX for padding
-    std::vector<uint32_t> rowDensityInMixture; // [nTiles*16]
+    std::vector<uint32_t> rowDensityInMixture; // [nTiles*rows]
+    uint32_t              rows = kTileRows;        // densities per tile
     uint32_t              maxEntriesPerMixture = 0;
 };
 
@@ -94,12 +95,14 @@ struct PreparedFloat {
     // two f16 pieces, hi + lo; a row is  sum_d [mh*xh + mh*xl + ml*xh]  +  sum_s limb_s * 2^(b_s)
     bool                  split    = false;
     uint32_t              kSteps16 = 0;    // K/32 steps of v_mfma_f32_16x16x32_f16
-    std::vector<uint16_t> tileH;           // [nTiles][kSteps16][64 lanes][8] f16 bits
+    std::vector<uint16_t> tileH;           // [nTiles][kSteps16][64 lanes][8] f16 bits (kSteps16: K steps of the
+                                           // tile's MFMA, 32 wide for 16-row tiles, 16 wide for 32-row tiles)
     std::vector<float>    dimScale;        // [dimension]: 2^a_d, x'' = x' * 2^a_d, m'' = -2 m' / 2^a_d
     int32_t               limbExp[4] = {0, 0, 0, 0};  // b_s: the frame side of limb s is 2^(b_s - e_frame)
     // split kernel keys: the low splitKeyBits mantissa bits hold (tile in mixture << 2 | row slot);
     // every mixture has an even number of tiles (pad tiles repeat the mixture's first row)
     uint32_t              splitKeyBits = 0;
+    uint32_t              splitRows    = 16;  // tile height: 16 (16x16x32 MFMA, tile pairs) or 32 (32x32x16)
 };
 
 
@@ -113,6 +116,6 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
 // wantSplit: lay the model out for the split-f16 kernel when it applies (one covariance,
 // 3*dimension+7 <= 256, row constants below 2^30); out.split says whether it did.
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
-                         ShardRange shard, PreparedFloat& out, bool wantSplit = false);
+                         ShardRange shard, PreparedFloat& out, bool wantSplit = false, uint32_t splitRowsWanted = 0);
 
 }  // namespace rasr_gmm

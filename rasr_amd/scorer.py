@@ -30,7 +30,8 @@ class Scorer:
 
     def __init__(self, mixture_set: MixtureSet, scorer_type="SIMD-diagonal-maximum", max_frames: int = 4096,
                  device: int = 0, mixture_weight_scale: float = 1.0, gaussian_scale: float = 1.0,
-                 score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None, native_f32: bool = False):
+                 score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None, native_f32: bool = False,
+                 split_tile16: bool = False, split_tile32: bool = False):
         self._lib = _capi.load_library()
         self.mixture_set = mixture_set
         self.type = _type_id(scorer_type)
@@ -41,6 +42,10 @@ class Scorer:
         cfg.score_scale = score_scale
         if native_f32:  # float types: the f32-MFMA kernel instead of the split-f16 one
             cfg.flags |= _capi.GMM_FLAG_NATIVE_F32
+        if split_tile16:  # split-f16 kernel: force 16-density tiles
+            cfg.flags |= _capi.GMM_FLAG_SPLIT_TILE16
+        if split_tile32:  # split-f16 kernel: force 32-density tiles (mixtures <= 512 densities, D <= 51)
+            cfg.flags |= _capi.GMM_FLAG_SPLIT_TILE32
         if mixture_range is not None:
             cfg.mixture_begin, cfg.mixture_end = int(mixture_range[0]), int(mixture_range[1])
         self.max_frames = int(max_frames)

@@ -3,7 +3,8 @@
 
 Each variant runs in its own subprocess (RASR_GMM_LIB=<so>); rounds are interleaved
 (v1 v2 ... v1 v2 ...) and the median / min kernel time per variant is reported.
-usage: ab_bench.py --mode fp32|simd --rounds 3 lib1.so lib2.so ...
+usage: ab_bench.py --mode fp32|simd --rounds 3 lib1.so lib2.so[:split16|:split32] ...
+(":split16" / ":split32" run that library with GMM_FLAG_SPLIT_TILE16 / _TILE32)
 """
 import argparse
 import json
@@ -20,9 +21,11 @@ sys.path.insert(0, os.environ["ROOT"])
 import torch, rasr_amd as ra
 mode = os.environ["MODE"]; F = int(os.environ["FRAMES"])
 kind = "diagonal-maximum" if mode == "fp32" else "SIMD-diagonal-maximum"
-ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
-sc = ra.Scorer(ms, kind, max_frames=F)
-fr = torch.from_numpy(ra.synthetic_frames(F, 39, seed=5)).cuda()
+D = int(os.environ.get("DIM", "39"))
+ms = ra.synthetic_mixture_set(5000, 160, D, seed=2024)
+sc = ra.Scorer(ms, kind, max_frames=F, split_tile16=os.environ.get("SPLIT") == "16",
+               split_tile32=os.environ.get("SPLIT") == "32")
+fr = torch.from_numpy(ra.synthetic_frames(F, D, seed=5)).cuda()
 out = torch.empty((5000, F), dtype=torch.float32, device="cuda")
 best = torch.empty((5000, F), dtype=torch.int32, device="cuda")
 for _ in range(3): sc.score_device(fr, out, best)
@@ -39,6 +42,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--frames", type=int, default=0)
+    ap.add_argument("--dim", type=int, default=39)
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     frames = a.frames or (8192 if a.mode == "fp32" else 32768)
@@ -46,8 +50,9 @@ def main():
     sums = {}
     for _ in range(a.rounds):
         for lib in a.libs:
-            env = dict(os.environ, RASR_GMM_LIB=os.path.abspath(lib), ROOT=ROOT, MODE=a.mode, FRAMES=str(frames),
-                       STEPS=str(a.steps))
+            path, _, opt = lib.partition(":")
+            env = dict(os.environ, RASR_GMM_LIB=os.path.abspath(path), ROOT=ROOT, MODE=a.mode, FRAMES=str(frames),
+                       STEPS=str(a.steps), DIM=str(a.dim), SPLIT=opt.replace("split", ""))
             p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 print(lib, "FAILED", p.stderr[-2000:])

@@ -3,9 +3,10 @@
 Tolerances (written here, per the north star):
   * SIMD-diagonal-maximum, batch-diagonal-maximum-int: BIT-EXACT scores and best densities.
   * diagonal-maximum, batch-diagonal-maximum-float: |gpu - ref| <= 1e-4 * max(1, |ref|); best density
-    identical wherever the two best candidates differ by more than that tolerance.  Both float
-    kernels are checked: the default split-f16 kernel (f32 operands as two f16 pieces on
-    v_mfma_f32_16x16x32_f16) and the f32-MFMA kernel (native_f32=True).
+    identical wherever the two best candidates differ by more than that tolerance.  Every float
+    kernel is checked: the split-f16 kernel (f32 operands as two f16 pieces) with 32-density tiles
+    (v_mfma_f32_32x32x16_f16, the default for mixtures of <= 512 densities) and with 16-density
+    tiles (v_mfma_f32_16x16x32_f16, split_tile16=True), and the f32-MFMA kernel (native_f32=True).
 """
 import numpy as np
 import pytest
@@ -16,7 +17,10 @@ import rasr_amd as ra
 pytestmark = pytest.mark.gpu
 
 REL_TOL = 1e-4
-FLOAT_KERNELS = [pytest.param(False, id="split"), pytest.param(True, id="native")]
+FLOAT_KERNELS = [pytest.param({"split_tile16": True}, id="split16"), pytest.param({"split_tile32": True}, id="split32"),
+                 pytest.param({"native_f32": True}, id="native")]
+KIND_OPTS = {"": {}, "native": {"native_f32": True}, "split16": {"split_tile16": True},
+             "split32": {"split_tile32": True}}
 
 
 def _gpu_scores(ms, frames, kind, **kw):
@@ -98,46 +102,53 @@ def _check_float(gpu_s, gpu_b, ref_s, ref_b, ms, frames, om, mixture_offset=0, m
         assert abs(a - b) <= REL_TOL * max(1.0, abs(b)), f"mixture {e} frame {t}: {gpu_b[e, t]} vs {ref_b[e, t]}"
 
 
-@pytest.mark.parametrize("native", FLOAT_KERNELS)
+@pytest.mark.parametrize("kopts", FLOAT_KERNELS)
 @pytest.mark.parametrize("case", QUANT_CASES)
-def test_diagonal_maximum_fp32(gpu, case, native):
+def test_diagonal_maximum_fp32(gpu, case, kopts):
     m, k, d, c, w, f = case
     ms = _model(m, k, d, c, w)
     frames = ra.synthetic_frames(f, d, seed=13)
     om = oracle.OracleFloat(ms)
     ref_s, ref_b = om.score(frames, n_threads=8)
-    s, b = _gpu_scores(ms, frames, "diagonal-maximum", native_f32=native)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum", **kopts)
     _check_float(s, b, ref_s, ref_b, ms, frames, om)
 
 
-@pytest.mark.parametrize("native", FLOAT_KERNELS)
-def test_diagonal_maximum_scales(gpu, native):
+@pytest.mark.parametrize("kopts", FLOAT_KERNELS)
+def test_diagonal_maximum_scales(gpu, kopts):
     ms = _model(50, 12, 39, 1, "random")
     frames = ra.synthetic_frames(300, 39, seed=14)
     ref_s, ref_b = oracle.OracleFloat(ms, mixture_weight_scale=0.7, gaussian_scale=1.3).score(frames, 8)
     s, b = _gpu_scores(ms, frames, "diagonal-maximum", mixture_weight_scale=0.7, gaussian_scale=1.3,
-                       native_f32=native)
+                       **kopts)
     _check_float(s, b, ref_s, ref_b, ms, frames, None, mws=0.7, gs=1.3)
 
 
-@pytest.mark.parametrize("native", FLOAT_KERNELS)
+@pytest.mark.parametrize("kopts", FLOAT_KERNELS)
 @pytest.mark.parametrize("case", [q for q in QUANT_CASES if q[3] == 1])
-def test_batch_float_fp32(gpu, case, native):
+def test_batch_float_fp32(gpu, case, kopts):
     m, k, d, c, w, f = case
     ms = _model(m, k, d, c, w)
     frames = ra.synthetic_frames(f, d, seed=15)
     ref = oracle.batch_float_score(ms, frames, n_threads=8)
-    s, _ = _gpu_scores(ms, frames, "batch-diagonal-maximum-float", native_f32=native)
+    s, _ = _gpu_scores(ms, frames, "batch-diagonal-maximum-float", **kopts)
     _assert_close(s, ref)
 
 
 def test_float_kernel_selection(gpu):
-    """One covariance -> split-f16 kernel; several covariances or GMM_FLAG_NATIVE_F32 -> f32 MFMA."""
+    """One covariance -> split-f16 kernel: 32-density tiles where their 16-wide K steps save a step
+    (D = 45) and mixtures have <= 512 densities, else 16-density tiles; several covariances or
+    GMM_FLAG_NATIVE_F32 -> f32 MFMA."""
     assert ra.Scorer(_model(10, 4, 39, 1, "random"), "diagonal-maximum").main_kernel() == "scoreSplit"
     assert ra.Scorer(_model(10, 4, 39, 1, "random"), "batch-diagonal-maximum-float").main_kernel() == "scoreSplit"
+    assert ra.Scorer(_model(10, 4, 45, 1, "random"), "diagonal-maximum").main_kernel() == "scoreSplit32"
+    assert ra.Scorer(_model(10, 4, 45, 1, "random"), "diagonal-maximum", split_tile16=True).main_kernel() == "scoreSplit"
+    assert ra.Scorer(_model(10, 4, 39, 1, "random"), "diagonal-maximum", split_tile32=True).main_kernel() == "scoreSplit32"
+    assert ra.Scorer(_model(4, 600, 45, 1, "random"), "diagonal-maximum").main_kernel() == "scoreSplit"
+    assert ra.Scorer(_model(10, 4, 60, 1, "random"), "diagonal-maximum", split_tile32=True).main_kernel() == "scoreSplit"
     assert ra.Scorer(_model(10, 4, 39, 3, "random"), "diagonal-maximum").main_kernel() == "scoreF32"
     assert ra.Scorer(_model(10, 4, 39, 1, "random"), "diagonal-maximum", native_f32=True).main_kernel() == "scoreF32"
-    assert ra.Scorer(_model(10, 4, 90, 1, "random"), "diagonal-maximum").main_kernel() == "scoreF32"  # 3D+4 > 256
+    assert ra.Scorer(_model(10, 4, 90, 1, "random"), "diagonal-maximum").main_kernel() == "scoreF32"  # 3D+7 > 256
 
 
 def test_split_accuracy_vs_f32_kernel(gpu):
@@ -147,15 +158,16 @@ def test_split_accuracy_vs_f32_kernel(gpu):
     frames = ra.synthetic_frames(1024, 39, seed=31)
     ref_s, _ = oracle.OracleFloat(ms).score(frames, n_threads=8)
     errs = {}
-    for native in (False, True):
-        s, _ = _gpu_scores(ms, frames, "diagonal-maximum", native_f32=native)
-        errs[native] = float((np.abs(s.astype(np.float64) - ref_s) / np.maximum(1.0, np.abs(ref_s))).max())
-    print("max rel err split %.3g native %.3g" % (errs[False], errs[True]))
-    assert errs[False] <= 1e-5 and errs[False] <= 8 * max(errs[True], 2.0 ** -22)
+    for name, opts in KIND_OPTS.items():
+        s, _ = _gpu_scores(ms, frames, "diagonal-maximum", **opts)
+        errs[name] = float((np.abs(s.astype(np.float64) - ref_s) / np.maximum(1.0, np.abs(ref_s))).max())
+    print("max rel err split16 %.3g split32 %.3g native %.3g" % (errs["split16"], errs["split32"], errs["native"]))
+    for name in ("", "split16", "split32"):  # keys drop <= 8 low mantissa bits: within 2^-17 of the f32 kernel's class
+        assert errs[name] <= 1e-5 and errs[name] <= 16 * max(errs["native"], 2.0 ** -22)
 
 
-@pytest.mark.parametrize("native", FLOAT_KERNELS)
-def test_float_extreme_frames(gpu, native):
+@pytest.mark.parametrize("kopts", FLOAT_KERNELS)
+def test_float_extreme_frames(gpu, kopts):
     """Per-frame exponent handling: huge, tiny, zero and mixed-magnitude frames."""
     ms = _model(30, 9, 39, 1, "random")
     frames = ra.synthetic_frames(64, 39, seed=32)
@@ -166,7 +178,7 @@ def test_float_extreme_frames(gpu, native):
     frames[4] *= 3e4
     frames[5, 7] = 1e18
     ref_s, ref_b = oracle.OracleFloat(ms).score(frames)
-    s, b = _gpu_scores(ms, frames, "diagonal-maximum", native_f32=native)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum", **kopts)
     _check_float(s, b, ref_s, ref_b, ms, frames, None)
 
 
@@ -201,14 +213,14 @@ def test_edge_cases_simd(gpu):
     assert b[0, 0] == 0xFFFFFFFF  # empty mixture: bestDensity = (u32)size_t max
 
 
-@pytest.mark.parametrize("native", FLOAT_KERNELS)
-def test_edge_cases_float(gpu, native):
+@pytest.mark.parametrize("kopts", FLOAT_KERNELS)
+def test_edge_cases_float(gpu, kopts):
     ms = _edge_model()
     frames = ra.synthetic_frames(130, 39, seed=4)
     frames[0] *= 1000.0
     frames[2] = ms.means[4]
     ref_s, ref_b = oracle.OracleFloat(ms).score(frames)
-    s, b = _gpu_scores(ms, frames, "diagonal-maximum", native_f32=native)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum", **kopts)
     assert np.array_equal(s[0], ref_s[0])  # empty mixture: 0.5 * FLT_MAX
     _check_float(s[1:], b[1:], ref_s[1:], ref_b[1:], ms, frames, None, mixture_offset=1)
     assert b[4, 2] == 0  # exact tie between identical rows: the GPU keeps the lowest density index
@@ -256,18 +268,19 @@ def test_quantization_accessors(gpu):
     assert np.array_equal(sc.multiply_and_quantize(x), o.quantize_frame(x))
 
 
-@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum", "diagonal-maximum/native"])
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum", "diagonal-maximum/split32",
+                                  "diagonal-maximum/native"])
 def test_full_size_800k_subset(gpu, kind):
     """BASELINE config 2 model (5000 x 160 densities, D=39): GPU vs oracle on 96 frames."""
     import torch
     ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
     frames = ra.synthetic_frames(96, 39, seed=77)
-    kind, _, native = kind.partition("/")
+    kind, _, opt = kind.partition("/")
     if kind == "SIMD-diagonal-maximum":
         ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames, n_threads=16)
     else:
         ref_s, ref_b = oracle.OracleFloat(ms).score(frames, n_threads=16)
-    s, b = _gpu_scores(ms, frames, kind, **({"native_f32": True} if native else {}))
+    s, b = _gpu_scores(ms, frames, kind, **KIND_OPTS[opt])
     if kind == "SIMD-diagonal-maximum":
         _assert_bit_exact(s, ref_s)
         assert np.array_equal(b, ref_b)
@@ -276,7 +289,8 @@ def test_full_size_800k_subset(gpu, kind):
     del torch
 
 
-@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum", "diagonal-maximum/native"])
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum", "diagonal-maximum/split32",
+                                  "diagonal-maximum/native"])
 def test_full_size_batch_invariance(gpu, kind):
     """At the bench size (8192 frames x 800k densities): scoring the whole batch equals scoring
     it in uneven pieces, bit for bit (frames are independent; no cross-frame state)."""
@@ -284,8 +298,8 @@ def test_full_size_batch_invariance(gpu, kind):
     ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
     F = 8192
     frames = torch.from_numpy(ra.synthetic_frames(F, 39, seed=78)).to(gpu)
-    kind, _, native = kind.partition("/")
-    sc = ra.Scorer(ms, kind, max_frames=F, **({"native_f32": True} if native else {}))
+    kind, _, opt = kind.partition("/")
+    sc = ra.Scorer(ms, kind, max_frames=F, **KIND_OPTS[opt])
     M = sc.n_mixtures()
     full = torch.empty((M, F), dtype=torch.float32, device=gpu)
     fullb = torch.empty((M, F), dtype=torch.int32, device=gpu)
