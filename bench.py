@@ -46,8 +46,9 @@ SPLIT_PRODUCTS = 3                    # split-f16 kernel: mh*xh + mh*xl + ml*xh 
 MODES = {
     "fp32": ("diagonal-maximum", "f32"),
     "simd": ("SIMD-diagonal-maximum", "s8xs8->i32 (u8-quantized, bit-exact)"),
+    "sum": ("diagonal-sum", "f32"),  # log-sum-exp variant (GaussDiagonalSumFeatureScorer), --mode sum
 }
-DEFAULT_FRAMES = {"fp32": 8192, "simd": 32768}
+DEFAULT_FRAMES = {"fp32": 8192, "simd": 32768, "sum": 8192}
 
 
 def parse():
@@ -161,7 +162,7 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
                   - ms.mixture_offsets[scorer.shards[rank][0]]) if sharded else int(ms.n_entries)
     algo = 2.0 * args.dim * d_local * frames_per_gpu  # one multiply-add per (frame, density, component)
     kernel = sc.main_kernel()
-    split = kernel in ("scoreSplit", "scoreSplit32")
+    split = kernel in ("scoreSplit", "scoreSplit32", "scoreSplitSum")
     if split:
         # f32-accurate contraction on the f16 matrix cores: 3 f16 products per f32 multiply-add, so the
         # roofline for this arithmetic is the dense f16 peak / 3; the MFMA work actually issued covers
@@ -171,7 +172,7 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
         kq = 16 if kernel == "scoreSplit32" else 32
         k_issued = kq * ((3 * args.dim + 7 + kq - 1) // kq)
         issued = 2.0 * k_issued * d_local * frames_per_gpu
-    elif mode == "fp32":
+    elif mode in ("fp32", "sum"):
         peak = PEAK_F32_MFMA_TFLOPS
         issued = 2.0 * 4 * ((args.dim + 1 + 3) // 4) * d_local * frames_per_gpu
     else:
@@ -230,7 +231,7 @@ def main():
     res = run_mode(args, args.mode, ms, ws, rank, local, frames_per_gpu)
     extra = {}
     if not args.no_extra_mode:
-        other = "simd" if args.mode == "fp32" else "fp32"
+        other = "simd" if args.mode != "simd" else "fp32"
         r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_FRAMES[other])
         extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
                         "frames_per_gpu_per_step": r2["frames_per_gpu"], "dtype": r2["dtype"],

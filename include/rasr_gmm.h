@@ -37,7 +37,11 @@ typedef enum {
     GMM_BATCH_DIAGONAL_MAXIMUM_INT   = 3, /* "batch-diagonal-maximum-int"   BatchFeatureScorer.cc:293-474 */
     GMM_BATCH_DIAGONAL_MAXIMUM_FAST  = 4, /* "batch-diagonal-maximum-fast"  BatchFeatureScorer.cc:537-604 */
     GMM_DIAGONAL_MAXIMUM             = 5, /* "diagonal-maximum"   GaussDiagonalMaximumFeatureScorer.cc */
-    GMM_SIMD_DIAGONAL_MAXIMUM        = 9  /* "SIMD-diagonal-maximum" SimdFeatureScorer.cc            */
+    GMM_SIMD_DIAGONAL_MAXIMUM        = 9, /* "SIMD-diagonal-maximum" SimdFeatureScorer.cc            */
+    GMM_DIAGONAL_SUM                 = 12 /* diagonalSum: GaussDiagonalSumFeatureScorer
+                                             (GaussDiagonalMaximumFeatureScorer.cc:221-298), no
+                                             registration string in the reference factory; here
+                                             "diagonal-sum".  One covariance, split-f16 kernel only. */
 } gmm_scorer_type;
 
 /* In-memory Mm::MixtureSet (src/Mm/MixtureSet.hh:140-212).  Replaces what the

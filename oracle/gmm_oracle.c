@@ -462,6 +462,71 @@ int orc_float_score(const orc_float_model* m, const orc_mixture_set* ms, const f
 }
 
 /* ------------------------------------------------------------------------- */
+/* diagonal-sum: GaussDiagonalSumFeatureScorer (GaussDiagonalMaximumFeatureScorer.cc:221-298)   */
+/* ------------------------------------------------------------------------- */
+static void orc_float_sum_frames(void* p, uint32_t t0, uint32_t t1) {
+    const orc_float_ctx*   x  = (const orc_float_ctx*)p;
+    const orc_float_model* m  = x->m;
+    const orc_mixture_set* ms = x->ms;
+    const uint32_t         D  = m->dimension;
+    uint32_t               t, e, i, maxn = 1;
+    float*                 sc;
+    for (e = 0; e < ms->n_mixtures; ++e)
+        if (ms->mixture_offsets[e + 1] - ms->mixture_offsets[e] > maxn)
+            maxn = ms->mixture_offsets[e + 1] - ms->mixture_offsets[e];
+    sc = (float*)malloc(sizeof(float) * maxn);  /* scores_ (cc:224, maximumNumberOfDensities) */
+    for (t = t0; t < t1; ++t) {
+        const float* f = x->frames + (size_t)t * x->frame_stride;
+        for (e = 0; e < ms->n_mixtures; ++e) {
+            uint32_t b = ms->mixture_offsets[e], n = ms->mixture_offsets[e + 1] - b;
+            float    bestScore   = FLT_MAX;  /* Core::Type<Score>::max */
+            uint64_t bestDensity = UINT64_MAX;
+            float    sumExp      = 0;
+            /* calculateScoresAndNumberOfDensities -- cc:238-261: Score (f32) arithmetic */
+            for (i = 0; i < n; ++i) {
+                uint32_t dns   = ms->mixture_densities[b + i];
+                uint32_t cov   = ms->density_covariance[dns];
+                float    score = m->minus2_log_weight[b + i] + m->log_norm[cov] +
+                              orc_float_distance(f, ms->means + (size_t)ms->density_mean[dns] * D,
+                                                 m->isv + (size_t)cov * D, D);
+                sc[i] = (float)(0.5 * score);
+            }
+            /* calculateScoreAndDensity -- cc:263-286 */
+            for (i = 0; i < n; ++i)
+                if (bestScore > sc[i]) {
+                    bestScore   = sc[i];
+                    bestDensity = i;
+                }
+            for (i = 0; i < n; ++i)
+                sumExp += expf(bestScore - sc[i]);
+            {
+                size_t o = (size_t)e * x->n_frames + t;
+                if (x->scores)
+                    x->scores[o] = bestScore - logf(sumExp);
+                if (x->best)
+                    x->best[o] = (uint32_t)bestDensity;
+            }
+        }
+    }
+    free(sc);
+}
+
+int orc_float_sum_score(const orc_float_model* m, const orc_mixture_set* ms, const float* frames,
+                        uint32_t n_frames, uint32_t frame_stride, float* scores, uint32_t* best_density,
+                        int n_threads) {
+    orc_float_ctx x;
+    x.m = m;
+    x.ms = ms;
+    x.frames = frames;
+    x.n_frames = n_frames;
+    x.frame_stride = frame_stride;
+    x.scores = scores;
+    x.best = best_density;
+    orc_parallel_frames(orc_float_sum_frames, &x, n_frames, n_threads);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* batch-diagonal-maximum-int                                                  */
 /* ------------------------------------------------------------------------- */
 typedef struct {

@@ -97,6 +97,10 @@ void orc_float_free(orc_float_model* m);
 int  orc_float_score(const orc_float_model* m, const orc_mixture_set* ms,
                      const float* frames, uint32_t n_frames, uint32_t frame_stride,
                      float* scores, uint32_t* best_density, int n_threads);
+/* diagonal-sum (GaussDiagonalSumFeatureScorer): same model as diagonal-maximum (inherited init) */
+int  orc_float_sum_score(const orc_float_model* m, const orc_mixture_set* ms,
+                         const float* frames, uint32_t n_frames, uint32_t frame_stride,
+                         float* scores, uint32_t* best_density, int n_threads);
 
 /* ---- batch-diagonal-maximum-int / -float (src/Mm/BatchFeatureScorer.cc) ---- */
 int orc_batch_int_score(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,

@@ -78,6 +78,8 @@ def load() -> ctypes.CDLL:
         "orc_float_free": (None, [ctypes.POINTER(OrcFloatModel)]),
         "orc_float_score": (ctypes.c_int, [ctypes.POINTER(OrcFloatModel), ctypes.POINTER(OrcMixtureSet), _vp,
                                            ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_int]),
+        "orc_float_sum_score": (ctypes.c_int, [ctypes.POINTER(OrcFloatModel), ctypes.POINTER(OrcMixtureSet), _vp,
+                                               ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_int]),
         "orc_batch_int_score": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, ctypes.c_uint32,
                                                ctypes.c_uint32, _vp, ctypes.c_int]),
         "orc_batch_float_score": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, ctypes.c_uint32,
@@ -189,14 +191,24 @@ class OracleFloat:
         except Exception:
             pass
 
+    _score_fn = "orc_float_score"
+
     def score(self, frames, n_threads: int = 1):
         f, n, stride = _frames(frames)
         M = self.d.n_mixtures
         scores = np.empty((M, n), np.float32)
         best = np.empty((M, n), np.uint32)
-        self.lib.orc_float_score(ctypes.byref(self.m), ctypes.byref(self.d.c), f.ctypes.data_as(_vp), n, stride,
-                                 scores.ctypes.data_as(_vp), best.ctypes.data_as(_vp), int(n_threads))
+        getattr(self.lib, self._score_fn)(ctypes.byref(self.m), ctypes.byref(self.d.c), f.ctypes.data_as(_vp), n,
+                                          stride, scores.ctypes.data_as(_vp), best.ctypes.data_as(_vp),
+                                          int(n_threads))
         return scores, best
+
+
+class OracleFloatSum(OracleFloat):
+    """diagonal-sum restated (GaussDiagonalSumFeatureScorer, GaussDiagonalMaximumFeatureScorer.cc:221-298):
+    -log sum_d exp(-s_d) with f32 density scores, best density as diagonal-maximum."""
+
+    _score_fn = "orc_float_sum_score"
 
 
 def batch_int_score(ms, frames, n_threads: int = 1):

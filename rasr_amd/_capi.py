@@ -24,6 +24,7 @@ BATCH_DIAGONAL_MAXIMUM_INT = 3
 BATCH_DIAGONAL_MAXIMUM_FAST = 4
 DIAGONAL_MAXIMUM = 5
 SIMD_DIAGONAL_MAXIMUM = 9
+DIAGONAL_SUM = 12  # diagonalSum (no registration string in the reference factory)
 
 SCORER_TYPES = {
     "batch-diagonal-maximum-float": BATCH_DIAGONAL_MAXIMUM_FLOAT,
@@ -31,6 +32,7 @@ SCORER_TYPES = {
     "batch-diagonal-maximum-fast": BATCH_DIAGONAL_MAXIMUM_FAST,
     "diagonal-maximum": DIAGONAL_MAXIMUM,
     "SIMD-diagonal-maximum": SIMD_DIAGONAL_MAXIMUM,
+    "diagonal-sum": DIAGONAL_SUM,
 }
 
 _u32p = ctypes.POINTER(ctypes.c_uint32)

@@ -251,20 +251,23 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.frameXX     = s->dFrameXX;
         a.frameExp    = s->dFrameExp;
         a.scores      = scores;
-        a.best        = s->flavor == Flavor::DiagonalMaximum ? best : nullptr;
+        a.best        = s->flavor != Flavor::BatchFloat ? best : nullptr;
         a.nFrames     = nFrames;
         a.nFramesPad  = s->nFramesPad;
         a.scoreStride = scoreStride;
         a.nChunks     = ct->nChunks;
         a.nFrameTiles = nFrameTiles;
         a.mixBase     = 0;
-        a.flavor      = s->flavor == Flavor::DiagonalMaximum ? 2 : 3;
+        a.flavor      = s->flavor == Flavor::DiagonalMaximum ? 2 : (s->flavor == Flavor::DiagonalSum ? 4 : 3);
         a.tileBits    = s->tileBits;
         a.offsetK0    = s->offsetK0;
         a.outScale    = s->cfg.score_scale;
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
-        GMM_HIP_CHECK(launchScoreSplit(a, s->splitRows, s->kSteps16, stream));
+        if (s->flavor == Flavor::DiagonalSum)
+            GMM_HIP_CHECK(launchScoreSplitSum(a, s->kSteps16, stream));
+        else
+            GMM_HIP_CHECK(launchScoreSplit(a, s->splitRows, s->kSteps16, stream));
         GMM_HIP_CHECK(span.end());
     }
     else {
@@ -306,6 +309,7 @@ Flavor flavorOf(gmm_scorer_type t, bool* quantized, bool* ok) {
         case GMM_BATCH_DIAGONAL_MAXIMUM_FAST: *quantized = true; return Flavor::BatchInt;
         case GMM_DIAGONAL_MAXIMUM: *quantized = false; return Flavor::DiagonalMaximum;
         case GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT: *quantized = false; return Flavor::BatchFloat;
+        case GMM_DIAGONAL_SUM: *quantized = false; return Flavor::DiagonalSum;
     }
     *ok = false;
     return Flavor::Simd;
@@ -573,7 +577,9 @@ int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLau
     if (nLaunches)
         *nLaunches = 2;
     if (name)
-        *name = s->quantized ? "scoreI8" : (s->split ? (s->splitRows == 32 ? "scoreSplit32" : "scoreSplit") : "scoreF32");
+        *name = s->quantized ? "scoreI8" : (s->split ? (s->flavor == Flavor::DiagonalSum ? "scoreSplitSum"
+                                                                         : (s->splitRows == 32 ? "scoreSplit32" : "scoreSplit"))
+                                                       : "scoreF32");
     return GMM_OK;
 }
 

@@ -86,7 +86,7 @@ struct SplitArgs {
     uint32_t*       best;
     uint32_t        nFrames, nFramesPad, scoreStride;
     uint32_t        nChunks, nFrameTiles, mixBase;
-    int             flavor;       // 2 diagonal-maximum, 3 batch-float
+    int             flavor;       // 2 diagonal-maximum, 3 batch-float, 4 diagonal-sum
     uint32_t        tileBits;
     float           offsetK0;
     float           outScale;
@@ -103,6 +103,7 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream);
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps, hipStream_t stream);
+hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps, hipStream_t stream);  // diagonal-sum, 16-row tiles
 constexpr uint32_t kSplit32MaxKSteps = 10;  // 32-row split kernel instantiated for K/16 <= 10 (D <= 51)
 hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 hipError_t launchScoreF32(const F32Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);

@@ -577,6 +577,236 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit32(SplitAr
     }
 }
 
+// ---------------------------------------------------------------------------
+// diagonal-sum (GaussDiagonalSumFeatureScorer, GaussDiagonalMaximumFeatureScorer.cc:221-298):
+// score = best - log sum_d exp(best - s_d) = -log sum_d exp(-s_d), best density as diagonal-maximum.
+// With u the MFMA value (2 s + K0, times 2^-e) and kap = 0.5 log2(e) 2^e of the frame,
+// exp(-s_d) = exp(K0/2) 2^(-kap u_d), so every lane keeps, per column block, a reference R (on the
+// kap u scale) and per slot S = sum 2^(R - kap u): one v_fma + v_exp + v_add per value beside the
+// (tag, min) key of diagonal-maximum.  R is re-based (a uniform branch, rare after the first pair of
+// a mixture) whenever a new value would put an exponent above 64; the final score is
+// R ln2 - K0/2 - ln(S) after the (R, S) pairs of the four lane groups are merged on a common R.
+// 16-row tiles, tile pairs, operands two pairs ahead as scoreSplit; no MFMA/VALU interleave.
+// ---------------------------------------------------------------------------
+template <bool BEST>
+__device__ __forceinline__ void emitMixtureSplitSum(const SplitArgs& a, const uint32_t (&best)[4][4],
+                                                    const float (&S)[4][4], const float (&R)[4], uint32_t m,
+                                                    uint32_t frame0, int lane, uint32_t g, uint32_t kmask) {
+    uint32_t k[4];
+    float    sum[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+        k[cb]   = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
+        sum[cb] = (S[cb][0] + S[cb][1]) + (S[cb][2] + S[cb][3]);
+    }
+    // merge (R, S) of two lane groups on the smaller R
+    const auto merge = [](float ra, float sa, float rb, float sb, float& r, float& sm) {
+        const float d = ra - rb;
+        r             = fminf(ra, rb);
+        sm            = d <= 0.0f ? __builtin_fmaf(sb, __builtin_amdgcn_exp2f(d), sa)
+                                  : __builtin_fmaf(sa, __builtin_amdgcn_exp2f(-d), sb);
+    };
+    uint32_t w[2], wg[2];
+    float    wr[2], ws[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const auto     r    = __builtin_amdgcn_permlane32_swap(k[p], k[p + 2], false, false);
+        const auto     rr   = __builtin_amdgcn_permlane32_swap(__float_as_uint(R[p]), __float_as_uint(R[p + 2]), false, false);
+        const auto     rs   = __builtin_amdgcn_permlane32_swap(__float_as_uint(sum[p]), __float_as_uint(sum[p + 2]), false, false);
+        const bool     take = r[1] < r[0];
+        w[p]                = take ? r[1] : r[0];
+        wg[p]               = (g & 1u) | (take ? 2u : 0u);
+        merge(__uint_as_float(rr[0]), __uint_as_float(rs[0]), __uint_as_float(rr[1]), __uint_as_float(rs[1]), wr[p], ws[p]);
+    }
+    const auto     rk   = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
+    const auto     rg   = __builtin_amdgcn_permlane16_swap(wg[0], wg[1], false, false);
+    const auto     rr   = __builtin_amdgcn_permlane16_swap(__float_as_uint(wr[0]), __float_as_uint(wr[1]), false, false);
+    const auto     rs   = __builtin_amdgcn_permlane16_swap(__float_as_uint(ws[0]), __float_as_uint(ws[1]), false, false);
+    const bool     take = rk[1] < rk[0];
+    const uint32_t key  = take ? rk[1] : rk[0];
+    const uint32_t grp  = take ? rg[1] : rg[0];
+    float          rf, sf;
+    merge(__uint_as_float(rr[0]), __uint_as_float(rs[0]), __uint_as_float(rr[1]), __uint_as_float(rs[1]), rf, sf);
+
+    const float kv   = __uint_as_float((key & ~kmask) | ((kmask + 1u) >> 1));
+    const bool  none = !(kv < 1e37f);  // empty mixture: R stays 1e30, S = 0 -> +inf, as the reference
+    // -log sum exp(-s_d) = R ln2 - K0/2 - ln S  (ln S = log2 S * ln2)
+    const float score = __fmul_rn(a.outScale, (rf - __builtin_amdgcn_logf(sf)) * 0.693147181f - 0.5f * a.offsetK0);
+    const uint32_t idx = none ? 0xffffffffu : ((((key & kmask) >> 2) << 4) | (grp << 2) | (key & 3u));
+    const uint32_t mo  = m - a.mixBase;
+    const uint32_t off = static_cast<uint32_t>(frame0 + lane) * 4u;
+    const auto rs_ = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                      static_cast<int>(a.nFrames * 4u), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs_, off, 0, 0);
+    if constexpr (BEST) {
+        const auto rb = __builtin_amdgcn_make_buffer_rsrc(a.best + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                         static_cast<int>(a.nFrames * 4u), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, 0);
+    }
+}
+
+template <int KS, bool BEST>
+__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(SplitArgs a,
+                                                                         const uint32_t* __restrict__ mixTileOff) {
+    constexpr int  NF   = 4;
+    const int      lane = threadIdx.x & 63;
+    const int      wave = threadIdx.x >> 6;
+    const uint32_t g    = static_cast<uint32_t>(lane) >> 4;
+    uint32_t       chunk, ft;
+    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
+        return;
+    const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
+    const uint32_t fb0    = frame0 / 16u;
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
+
+    const f16x8* th       = static_cast<const f16x8*>(a.tileH);
+    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS]) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+    };
+    const f16x8* fh = static_cast<const f16x8*>(a.frameH);
+    f16x8        B[NF][KS];
+    float        kap[NF];  // 0.5 log2(e) 2^e of the frame in column lane & 15 of block cb
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            B[cb][s] = fh[(static_cast<size_t>(fb0 + cb) * KS + s) * 64 + lane];
+        kap[cb] = ldexpf(0.721347520f, a.frameExp[frame0 + 16 * cb + (lane & 15)]);
+    }
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            asm volatile("" ::"v"(B[cb][s]));
+        asm volatile("" ::"v"(kap[cb]));
+    }
+    f16x8 R0[KS], R1[KS], R2[KS], R3[KS];
+    loadTile(T0, R0);
+    loadTile(T0 + 1, R1);
+    loadTile(T0 + 2, R2);
+    loadTile(T0 + 3, R3);
+
+    const uint32_t kmask = (1u << a.tileBits) - 1u;
+    uint32_t       vmask = ~kmask;
+    asm volatile("" : "+v"(vmask));
+
+    uint32_t   best[NF][4];
+    float      S[NF][4], Rf[NF];
+    const auto resetBest = [&]() {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            Rf[cb] = 1e30f;  // no reference yet: the first values re-base it
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                best[cb][r] = 0xffffffffu;
+                S[cb][r]    = 0.0f;
+            }
+        }
+    };
+    const auto chain = [&](const f16x8(&A)[KS], f32x4(&acc)[NF]) {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+            acc[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
+    };
+    const auto pairStep = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], uint32_t tl) {
+        f32x4 acc[2][NF];
+        chain(A0, acc[0]);
+        chain(A1, acc[1]);
+        uint32_t tagA[4], tagB[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            tagA[r] = (tl << 2) | r;
+            tagB[r] = ((tl + 1u) << 2) | r;
+            asm("" : "+s"(tagA[r]), "+s"(tagB[r]));
+        }
+        float t[2][NF][4];
+        bool  rebase = false;
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            float tmx = -3.40282347e+38f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t ka = (__float_as_uint(acc[0][cb][r]) & vmask) | tagA[r];
+                const uint32_t kb = (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
+                best[cb][r]       = umin3(best[cb][r], ka, kb);
+                t[0][cb][r]       = __builtin_fmaf(acc[0][cb][r], -kap[cb], Rf[cb]);
+                t[1][cb][r]       = __builtin_fmaf(acc[1][cb][r], -kap[cb], Rf[cb]);
+                tmx               = fmaxf(tmx, fmaxf(t[0][cb][r], t[1][cb][r]));
+            }
+            rebase = rebase || tmx > 64.0f;
+        }
+        if (__builtin_amdgcn_ballot_w64(rebase) != 0) {  // uniform: new reference R = kap * (best value so far)
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb) {
+                const uint32_t kb = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
+                const float    nr = kap[cb] * __uint_as_float(kb & vmask);
+                const float    f  = __builtin_amdgcn_exp2f(nr - Rf[cb]);
+                Rf[cb]            = nr;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    S[cb][r]    = S[cb][r] * f;
+                    t[0][cb][r] = __builtin_fmaf(acc[0][cb][r], -kap[cb], nr);
+                    t[1][cb][r] = __builtin_fmaf(acc[1][cb][r], -kap[cb], nr);
+                }
+            }
+        }
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                S[cb][r] += __builtin_amdgcn_exp2f(t[0][cb][r]) + __builtin_amdgcn_exp2f(t[1][cb][r]);
+    };
+
+    uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
+    resetBest();
+    const auto emit    = [&]() { emitMixtureSplitSum<BEST>(a, best, S, Rf, m, frame0, lane, g, kmask); };
+    const auto advance = [&](uint32_t tNext) {
+        ++m;
+        tBeg = tNext;
+        tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        while (m < m1 && tEnd == tNext) {
+            emit();
+            ++m;
+            tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        }
+    };
+    const auto finish = [&](uint32_t tNext) {
+        if (tNext == tEnd) {
+            emit();
+            resetBest();
+            advance(tNext);
+        }
+    };
+    while (m < m1 && tEnd == T0) {
+        emit();
+        ++m;
+        tEnd = m < m1 ? mixTileOff[m + 1] : T0;
+    }
+    uint32_t t = T0;
+    for (; t + 4 <= T1; t += 4) {
+        pairStep(R0, R1, t - tBeg);
+        loadTile(t + 4, R0);
+        loadTile(t + 5, R1);
+        finish(t + 2);
+        pairStep(R2, R3, t + 2 - tBeg);
+        loadTile(t + 6, R2);
+        loadTile(t + 7, R3);
+        finish(t + 4);
+    }
+    if (t < T1) {
+        pairStep(R0, R1, t - tBeg);
+        finish(t + 2);
+    }
+}
+
 }  // namespace dev
 
 hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
@@ -639,6 +869,32 @@ hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps16
         case 6: launchSplitK<6>(a, grid, stream); break;
         case 7: launchSplitK<7>(a, grid, stream); break;
         case 8: launchSplitK<8>(a, grid, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int KS>
+static void launchSplitSumK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
+    if (a.best)
+        hipLaunchKernelGGL((dev::scoreSplitSum<KS, true>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+    else
+        hipLaunchKernelGGL((dev::scoreSplitSum<KS, false>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+}
+
+hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream) {
+    const uint32_t grid = 8u * ((a.nChunks + 7u) / 8u) * a.nFrameTiles;
+    if (grid == 0)
+        return hipSuccess;
+    switch (kSteps16) {
+        case 1: launchSplitSumK<1>(a, grid, stream); break;
+        case 2: launchSplitSumK<2>(a, grid, stream); break;
+        case 3: launchSplitSumK<3>(a, grid, stream); break;
+        case 4: launchSplitSumK<4>(a, grid, stream); break;
+        case 5: launchSplitSumK<5>(a, grid, stream); break;
+        case 6: launchSplitSumK<6>(a, grid, stream); break;
+        case 7: launchSplitSumK<7>(a, grid, stream); break;
+        case 8: launchSplitSumK<8>(a, grid, stream); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

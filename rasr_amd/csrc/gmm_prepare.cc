@@ -339,7 +339,8 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
 
     // diagonal-maximum: covariance.scale(gaussianScale_ = sqrt(gaussian-scale)) (GDMFS.cc:51,83-84);
     // batch-float: unscaled (BatchFeatureScorer.cc:155-160).
-    const bool  dm = flavor == Flavor::DiagonalMaximum;
+    // diagonal-sum inherits init() from diagonal-maximum (GaussDiagonalMaximumFeatureScorer.hh:96)
+    const bool  dm = flavor == Flavor::DiagonalMaximum || flavor == Flavor::DiagonalSum;
     const float gs = dm ? static_cast<float>(std::sqrt(static_cast<double>(gaussianScale))) : 1.0f;
     out.isv.resize(static_cast<size_t>(C) * D);
     out.logNorm.resize(C);
@@ -432,7 +433,9 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
     const bool     fits32    = keyBits32 <= 8 && splitKSteps32(D) <= kSplit32MaxKSteps;
     const bool     saves32   = splitKSteps32(D) * 16 < splitKSteps(D) * 32;
     const bool     want32    = splitRowsWanted == 32 || (splitRowsWanted == 0 && saves32);
-    const uint32_t rows      = (fits32 && (want32 || keyBits16 > 8)) ? 32 : (keyBits16 <= 8 ? 16 : 0);
+    // diagonal-sum: 16-row tiles only (scoreSplitSum)
+    const uint32_t rows      = (flavor != Flavor::DiagonalSum && fits32 && (want32 || keyBits16 > 8))
+                                   ? 32 : (keyBits16 <= 8 ? 16 : 0);
     if (wantSplit && !out.foldNorm && splitKSteps(D) <= 8 && T > 0 && rows != 0) {
         std::vector<double> maxAbs(D, 0.0);
         double              maxConst = 0;
@@ -442,6 +445,11 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                     maxAbs[k] = std::max(maxAbs[k], std::fabs(static_cast<double>(m2[k])));
                 maxConst = std::max(maxConst, std::fabs(cst));
             }
+        // diagonal-sum adds every row of a mixture to its sum: padding rows (copies of a real row, which
+        // never win a minimum) must not add, so their constant is raised by 2^29 (2^(-0.72 * 2^29)
+        // underflows to 0 in the sum; the key never wins)
+        const double padBias = flavor == Flavor::DiagonalSum ? std::ldexp(1.0, 29) : 0.0;
+        maxConst += padBias;
         bool finite = std::isfinite(maxConst);
         for (double v : maxAbs)
             finite = finite && std::isfinite(v);
@@ -527,8 +535,10 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                 for (uint32_t r = 0; r < rows; ++r) {
                     std::fill(row.begin(), row.end(), 0);
                     // a padding row repeats row 0 of its tile (a pad tile: of its mixture's first tile)
-                    if (entryValues(out.tiling.rowEntry[static_cast<size_t>(t) * rows + r], m2.data(), cst) ||
-                        entryValues(fillEntry[t], m2.data(), cst)) {
+                    const bool real = entryValues(out.tiling.rowEntry[static_cast<size_t>(t) * rows + r], m2.data(), cst);
+                    if (real || entryValues(fillEntry[t], m2.data(), cst)) {
+                        if (!real)
+                            cst += padBias;
                         for (uint32_t k = 0; k < D; ++k) {
                             const float    v  = static_cast<float>(m2[k] * inv[k]);  // exact: power of two
                             const uint16_t hi = h16(v);
@@ -557,6 +567,10 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
             }
         }
     }
+
+    if (flavor == Flavor::DiagonalSum && !out.split)
+        return "diagonal-sum runs on the split-f16 kernel only: one covariance, dimension <= 83, "
+               "<= 1024 densities per mixture";
 
     // ---- native f32 layout ----
     if (!out.split) {

@@ -50,7 +50,7 @@ float   refQuantizationScalingFactor(float minv, float maxv); // SimdFeatureScor
 int32_t refTruncF32(float x);                  // (s32)float, cvttss2si
 int32_t refTruncF64(double x);                 // (s32)double, cvttsd2si
 
-enum class Flavor : int { Simd = 0, BatchInt = 1, DiagonalMaximum = 2, BatchFloat = 3 };
+enum class Flavor : int { Simd = 0, BatchInt = 1, DiagonalMaximum = 2, BatchFloat = 3, DiagonalSum = 4 };
 
 struct Tiling {
     uint32_t              nTiles = 0;

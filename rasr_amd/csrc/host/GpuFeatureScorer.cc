@@ -87,6 +87,7 @@ static bool typeOf(const std::string& name, gmm_scorer_type* t, bool* assigning,
     } const table[] = {
             {"SIMD-diagonal-maximum", GMM_SIMD_DIAGONAL_MAXIMUM, true, false},
             {"diagonal-maximum", GMM_DIAGONAL_MAXIMUM, true, false},
+            {"diagonal-sum", GMM_DIAGONAL_SUM, true, false},
             {"batch-diagonal-maximum-int", GMM_BATCH_DIAGONAL_MAXIMUM_INT, false, true},
             {"batch-diagonal-maximum-fast", GMM_BATCH_DIAGONAL_MAXIMUM_FAST, false, true},
             {"batch-diagonal-maximum-float", GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT, false, true},
