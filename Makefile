@@ -17,11 +17,11 @@ HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc
 HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh \
-            $(SRC)/host/GpuFeatureScorer.hh include/rasr_gmm_io.h
+            $(SRC)/host/GpuFeatureScorer.hh include/rasr_gmm_io.h include/rasr_nn.h $(SRC)/nn_kernels.hh
 
 LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
-            $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o
+            $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 all: $(LIB) $(DRIVER) oracle
@@ -37,6 +37,15 @@ $(BUILD)/gmm_kernels_f32.o: $(SRC)/gmm_kernels_f32.hip $(HDRS)
 $(BUILD)/gmm_kernels_split.o: $(SRC)/gmm_kernels_split.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(SPLITFLAGS) -c $< -o $@
+
+# hybrid-DNN scorer (include/rasr_nn.h): bf16 MFMA GEMM per layer
+$(BUILD)/nn_kernels.o: $(SRC)/nn_kernels.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/nn_api.o: $(SRC)/nn_api.cc $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
 $(BUILD)/gmm_api.o: $(SRC)/gmm_api.cc $(HDRS)
 	@mkdir -p $(BUILD)

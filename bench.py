@@ -47,8 +47,11 @@ MODES = {
     "fp32": ("diagonal-maximum", "f32"),
     "simd": ("SIMD-diagonal-maximum", "s8xs8->i32 (u8-quantized, bit-exact)"),
     "sum": ("diagonal-sum", "f32"),  # log-sum-exp variant (GaussDiagonalSumFeatureScorer), --mode sum
+    "nn": ("nn-batch-feature-scorer", "bf16 x bf16 -> f32 (MFMA), f32 bias/activation"),  # config 5, --mode nn
 }
-DEFAULT_FRAMES = {"fp32": 8192, "simd": 32768, "sum": 8192}
+DEFAULT_FRAMES = {"fp32": 32768, "simd": 32768, "sum": 32768, "nn": 32768}  # frames per GPU per step (batch)
+# BASELINE config 5 network (hybrid DNN): 11 x 39 spliced MFCC input, 6 sigmoid layers of 2048, 5000 classes
+NN_DIMS = [429] + [2048] * 6 + [5000]
 
 
 def parse():
@@ -207,6 +210,52 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
     return res
 
 
+def run_nn(args, ws, rank, local, frames_per_gpu):
+    """Nn::BatchFeatureScorer drop-in (rasr_amd.nn): one bf16 MFMA GEMM per layer, bias + activation fused;
+    a step scores frames_per_gpu frames on every rank (frame-sharded replicas, no collective)."""
+    import numpy as np
+    import torch
+    import rasr_amd as ra
+    from rasr_amd import nn
+    dev = torch.device("cuda", local)
+    layers = nn.synthetic_network(NN_DIMS, "sigmoid", seed=2024)
+    lp = np.full(NN_DIMS[-1], -np.log(NN_DIMS[-1]), np.float32)
+    sc = nn.NnScorer(layers, log_prior=lp, prior_scale=1.0, max_frames=frames_per_gpu, device=local)
+    frames = torch.from_numpy(ra.synthetic_frames(frames_per_gpu, NN_DIMS[0], seed=1000 + rank)).to(dev)
+    scores = torch.empty((NN_DIMS[-1], frames_per_gpu), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        sc.score_device(frames, scores, stream)
+    barrier(ws)
+    sc.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sc.score_device(frames, scores, stream)
+    barrier(ws)
+    dt = time.perf_counter() - t0
+    kms, nl = sc.kernel_time(reset=True)
+    sc.set_timing(False)
+    dt_max = max_over_ranks(dt, ws)
+    kms_avg = max_over_ranks(kms / max(nl, 1), ws)
+    algo = 2.0 * sum(a * b for a, b in zip(NN_DIMS[:-1], NN_DIMS[1:])) * frames_per_gpu
+    pad = lambda x, q: (x + q - 1) // q * q  # GEMM tiles: outputs to 128, the input to 64
+    kp = [pad(NN_DIMS[0], 64)] + [pad(d, 128) for d in NN_DIMS[1:-1]]
+    issued = 2.0 * sum(k * pad(m, 128) for k, m in zip(kp, NN_DIMS[1:])) * pad(frames_per_gpu, 128)
+    sec = kms_avg * 1e-3
+    return {
+        "value": ws * frames_per_gpu * args.steps / dt_max,
+        "ms_per_step": dt_max / args.steps * 1e3,
+        "dtype": MODES["nn"][1],
+        "frames_per_gpu": frames_per_gpu,
+        "roofline": {
+            "bound": "mfma", "achieved": algo / sec / 1e12, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": algo / sec / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None, "kernel": "nnGemm",
+            "kernel_ms": kms_avg, "algorithmic_flop_per_launch": algo, "issued_mfma_flop_per_launch": issued,
+            "issued_mfma_tflops": issued / sec / 1e12,
+        },
+    }
+
+
 def cpu_baseline(args, ms):
     import oracle
     import rasr_amd as ra
@@ -227,11 +276,27 @@ def main():
     import rasr_amd as ra
     ws, rank, local = dist_setup()
     frames_per_gpu = args.frames or DEFAULT_FRAMES[args.mode]
+    if args.mode == "nn":
+        res = run_nn(args, ws, rank, local, frames_per_gpu)
+        if rank == 0:
+            print(json.dumps({
+                "metric": "frames/sec scored, hybrid-DNN posteriors (Nn::BatchFeatureScorer)", "value": res["value"],
+                "unit": "frames/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": res["dtype"], "data": "synthetic (random-init network, frames N(0,1))",
+                "config": {"workload": "hybrid DNN " + "-".join(map(str, NN_DIMS)) + " sigmoid, 5000 classes",
+                           "frames_per_gpu_per_step": frames_per_gpu,
+                           "parallelism": f"frame-sharded replicas x{ws}"},
+                "roofline": res["roofline"], "cpu_baseline": None}), flush=True)
+        if ws > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     ms = ra.synthetic_mixture_set(args.mixtures, args.densities, args.dim, seed=2024)
     res = run_mode(args, args.mode, ms, ws, rank, local, frames_per_gpu)
     extra = {}
     if not args.no_extra_mode:
-        other = "simd" if args.mode != "simd" else "fp32"
+        other = "simd" if args.mode != "simd" else "fp32"  # (nn returned above)
         r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_FRAMES[other])
         extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
                         "frames_per_gpu_per_step": r2["frames_per_gpu"], "dtype": r2["dtype"],

@@ -143,7 +143,10 @@ int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
         *out = &it->second;
         return GMM_OK;
     }
-    const uint32_t kTargetBlocks = 8192;
+#ifndef GMM_TARGET_BLOCKS
+#define GMM_TARGET_BLOCKS 8192
+#endif
+    const uint32_t kTargetBlocks = GMM_TARGET_BLOCKS;
     uint32_t       target        = std::max<uint32_t>(1, (kTargetBlocks + nFrameTiles - 1) / nFrameTiles);
     target                       = std::min<uint32_t>(target, std::max<uint32_t>(1, s->nMix));
     const uint32_t T             = s->nTiles;

@@ -1,0 +1,34 @@
+// nn_kernels.hh -- launch interface of the hybrid-DNN scorer kernels (nn_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rasr_nn {
+
+constexpr uint32_t kNnTileM = 128;  // output units per workgroup tile
+constexpr uint32_t kNnTileN = 128;  // frames per workgroup tile
+constexpr uint32_t kNnTileK = 64;   // K per pipeline stage
+
+// One layer: Out = act(A . B^T + bias) with A = W^T [Mpad][Kpad] (bf16 bits), B = layer input
+// [Npad][Kpad] (bf16 bits, frame-major).  Hidden layers store Y [Npad][Mpad] bf16 (the next
+// layer's B); the top layer stores scores[m * scoreStride + n] = -(A . B^T + bias)[m][n] for
+// m < M, n < nFrames.
+struct NnGemmArgs {
+    const uint16_t* A;
+    const uint16_t* B;
+    const float*    bias;      // [Mpad]
+    uint16_t*       Y;         // hidden layers
+    float*          scores;    // top layer
+    uint32_t        Mpad, Kpad, Npad, M, nFrames, scoreStride;
+    int             act;       // nn_activation
+    float           gamma;
+    int             top;
+};
+
+hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
+                                uint32_t Kpad, uint16_t* X, hipStream_t stream);
+hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream);
+
+}  // namespace rasr_nn

@@ -1,0 +1,81 @@
+"""Hybrid-DNN scorer (rasr_amd.nn, include/rasr_nn.h): the MI355X drop-in for Nn::BatchFeatureScorer
+(src/Nn/BatchFeatureScorer.cc), checked against oracle/nn_oracle.py.
+
+Tolerances (bf16 MFMA, f32 accumulation, BASELINE config 5):
+  * against the bf16 contract (oracle.forward_bf16: the same bf16 roundings, exact sums):
+    |gpu - ref| <= 2e-3 * (1 + |ref|) -- accumulation order and device exp/tanh only;
+  * against the reference's f32 arithmetic (oracle.forward_f32): |gpu - ref| <= 5e-2 * (1 + |ref|),
+    the bf16 rounding of weights and activations (measured max printed by the test).
+"""
+import numpy as np
+import pytest
+
+import rasr_amd as ra
+from oracle import nn_oracle
+from rasr_amd import nn
+
+
+def _err(a, ref):
+    return float((np.abs(a.astype(np.float64) - ref) / (1.0 + np.abs(ref))).max())
+
+
+def test_oracle_prior_matches_library():
+    ms = ra.synthetic_mixture_set(30, ra.ragged_counts(30, 200, low=1, high=12, seed=3), 13, seed=3,
+                                  weights="random")
+    # unnormalised mixture weights: scale each mixture's weights differently
+    ms.mixture_log_weights[:] += np.repeat(np.log(np.arange(1, 31)), np.diff(ms.mixture_offsets))
+    assert np.allclose(nn.prior_from_mixture_set(ms), nn_oracle.prior_from_mixture_set(ms), atol=1e-6)
+
+
+def test_oracle_bf16_close_to_f32():
+    layers = nn.synthetic_network([39, 256, 256, 100], "sigmoid", seed=1)
+    frames = ra.synthetic_frames(50, 39, seed=2)
+    a = nn_oracle.forward_f32(layers, frames)
+    b = nn_oracle.forward_bf16(layers, frames)
+    assert _err(b, a.astype(np.float64)) < 5e-2
+    assert a.shape == (100, 50)
+
+
+ACTS = ["sigmoid", "tanh", "relu", "elu", "identity"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ACTS)
+@pytest.mark.parametrize("dims,frames", [([39, 256, 100], 300), ([429, 1000, 1000, 997], 517),
+                                          ([45, 128, 128, 128, 64], 128), ([16, 5000], 33)])
+def test_nn_scorer_gpu(gpu, act, dims, frames):
+    layers = nn.synthetic_network(dims, act, seed=len(dims) + frames)
+    x = ra.synthetic_frames(frames, dims[0], seed=frames)
+    lp = np.log(np.random.Generator(np.random.PCG64(4)).dirichlet(np.ones(dims[-1]))).astype(np.float32)
+    sc = nn.NnScorer(layers, log_prior=lp, prior_scale=0.6, max_frames=frames + 7)
+    assert sc.n_classes() == dims[-1] and sc.input_dim() == dims[0]
+    s = sc.score_host(x)
+    e16 = _err(s, nn_oracle.forward_bf16(layers, x, lp, 0.6).astype(np.float64))
+    e32 = _err(s, nn_oracle.forward_f32(layers, x, lp, 0.6).astype(np.float64))
+    print(f"{act} {dims}: vs bf16 contract {e16:.2e}, vs f32 {e32:.2e}")
+    assert e16 <= 2e-3
+    assert e32 <= 5e-2
+
+
+@pytest.mark.gpu
+def test_nn_scorer_device_strides_and_errors(gpu):
+    import torch
+    layers = nn.synthetic_network([39, 300, 200], "sigmoid", seed=9)
+    layers[0] = (layers[0][0], layers[0][1], "sigmoid", 0.5)  # SigmoidLayer "gamma"
+    layers[1] = (layers[1][0], None, "identity", 1.0)         # top layer without bias
+    x = ra.synthetic_frames(130, 39, seed=10)
+    sc = nn.NnScorer(layers, max_frames=130)
+    ref = nn_oracle.forward_bf16(layers, x).astype(np.float64)
+    padded = torch.zeros((130, 48), dtype=torch.float32, device=gpu)
+    padded[:, :39] = torch.from_numpy(x).to(gpu)
+    out = torch.full((200, 160), 7.0, dtype=torch.float32, device=gpu)
+    sc.score_device(padded, out)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert _err(o[:, :130], ref) <= 2e-3
+    assert (o[:, 130:] == 7.0).all()  # nothing written past n_frames
+    with pytest.raises(ra.GmmError):
+        sc.score_host(ra.synthetic_frames(131, 39, seed=1))  # more than max_frames
+    with pytest.raises(ra.GmmError):
+        nn.NnScorer([(np.ones((4, 5), np.float32), None, "relu", 1.0),
+                     (np.ones((6, 2), np.float32), None, "identity", 1.0)])  # 5 != 6
