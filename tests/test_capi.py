@@ -18,7 +18,8 @@ def _declared_functions():
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s+\**\s*(gmm_[a-z0-9_]+)\s*\(", src, re.M):
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s+\**\s*((?:gmm|nn)_[a-z0-9_]+)\s*\(",
+                             src, re.M):
             names.append(m.group(1))
     return sorted(set(names))
 
@@ -26,14 +27,25 @@ def _declared_functions():
 def test_header_declares_api():
     names = _declared_functions()
     assert "gmm_scorer_create" in names and "gmm_score_device" in names and len(names) >= 15
+    assert "nn_scorer_create" in names and "nn_score_device" in names  # include/rasr_nn.h
 
 
 def test_library_exports_every_declared_symbol(built):
+    from rasr_amd import nn
     lib = ctypes.CDLL(_capi.LIB_PATH)
     missing = [n for n in _declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
-    bound = {p[0] for p in _capi.PROTOTYPES}
+    bound = {p[0] for p in _capi.PROTOTYPES} | {p[0] for p in nn._PROTOTYPES}
     assert set(_declared_functions()) <= bound, set(_declared_functions()) - bound
+
+
+def test_nn_errors_without_device(built):
+    from rasr_amd import nn
+    lib = nn._lib()
+    h = ctypes.c_void_p()
+    assert lib.nn_scorer_create(None, 4, 0, ctypes.byref(h)) == -1
+    assert lib.nn_score_device(None, None, 1, 8, None, 1, None) == -1
+    assert lib.nn_scorer_destroy(None) == 0
 
 
 def test_library_is_native_gfx950(built):
