@@ -60,7 +60,11 @@ struct F32Args {
 #define GMM_SPLIT_NF 4  // the split kernel is written for 4 (emitMixtureSplit)
 #endif
 constexpr int      kSplitNF             = GMM_SPLIT_NF;  // column blocks of 16 frames per wave, split kernel
-constexpr uint32_t kSplitFramesPerBlock = kWavesPerBlock * kSplitNF * 16;
+#ifndef GMM_SPLIT_WAVES
+#define GMM_SPLIT_WAVES 4
+#endif
+constexpr uint32_t kSplitWaves          = GMM_SPLIT_WAVES;  // waves per workgroup of the split kernels
+constexpr uint32_t kSplitFramesPerBlock = kSplitWaves * kSplitNF * 16;
 
 constexpr uint32_t kSplitLimbs   = 4;
 constexpr uint32_t kSplitXXLimbs = 3;

@@ -212,7 +212,7 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
 // s_waitcnt vmcnt(0) draining the prefetch.
 // ---------------------------------------------------------------------------
 template <int KS, bool BEST>
-__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
+__global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
                                                                       const uint32_t* __restrict__ mixTileOff) {
     constexpr int  NF   = 4;
     const int      lane = threadIdx.x & 63;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs
     uint32_t       chunk, ft;
     if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
         return;
-    const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
+    const uint32_t frame0 = ft * kSplitFramesPerBlock + static_cast<uint32_t>(wave) * (NF * 16u);
     const uint32_t fb0    = frame0 / 16u;
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
     const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
@@ -433,7 +433,7 @@ __device__ __forceinline__ void emitMixtureSplit32(const SplitArgs& a, const uin
 }
 
 template <int KS, bool BEST>
-__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit32(SplitArgs a,
+__global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit32(SplitArgs a,
                                                                         const uint32_t* __restrict__ mixTileOff) {
     typedef float f32x16 __attribute__((ext_vector_type(16)));
     const int      lane = threadIdx.x & 63;
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplit32(SplitAr
     uint32_t       chunk, ft;
     if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
         return;
-    const uint32_t frame0 = ft * 256u + static_cast<uint32_t>(wave) * 64u;
+    const uint32_t frame0 = ft * kSplitFramesPerBlock + static_cast<uint32_t>(wave) * 64u;
     const uint32_t fb0    = frame0 / 32u;
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
     const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
@@ -646,7 +646,7 @@ __device__ __forceinline__ void emitMixtureSplitSum(const SplitArgs& a, const ui
 }
 
 template <int KS, bool BEST>
-__global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(SplitArgs a,
+__global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(SplitArgs a,
                                                                          const uint32_t* __restrict__ mixTileOff) {
     constexpr int  NF   = 4;
     const int      lane = threadIdx.x & 63;
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(256, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(SplitA
     uint32_t       chunk, ft;
     if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
         return;
-    const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
+    const uint32_t frame0 = ft * kSplitFramesPerBlock + static_cast<uint32_t>(wave) * (NF * 16u);
     const uint32_t fb0    = frame0 / 16u;
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
     const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
@@ -827,17 +827,17 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
 template <int KS>
 static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
     if (a.best)
-        hipLaunchKernelGGL((dev::scoreSplit<KS, true>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit<KS, true>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
     else
-        hipLaunchKernelGGL((dev::scoreSplit<KS, false>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit<KS, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
 }
 
 template <int KS>
 static void launchSplit32K(const SplitArgs& a, uint32_t grid, hipStream_t s) {
     if (a.best)
-        hipLaunchKernelGGL((dev::scoreSplit32<KS, true>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit32<KS, true>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
     else
-        hipLaunchKernelGGL((dev::scoreSplit32<KS, false>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit32<KS, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
 }
 
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps16, hipStream_t stream) {
@@ -877,9 +877,9 @@ hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps16
 template <int KS>
 static void launchSplitSumK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
     if (a.best)
-        hipLaunchKernelGGL((dev::scoreSplitSum<KS, true>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplitSum<KS, true>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
     else
-        hipLaunchKernelGGL((dev::scoreSplitSum<KS, false>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplitSum<KS, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
 }
 
 hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream) {
