@@ -28,6 +28,10 @@
 // This file: the quantized kernels (built with -mllvm -amdgpu-mfma-vgpr-form, see Makefile).
 #include "gmm_device.hh"
 
+#ifndef GMM_I8_INTERLEAVE
+#define GMM_I8_INTERLEAVE 4  // VALU per MFMA in a sched_group_barrier interleave of the pair step (0 = off; 4: +2 %, 6: -4 %)
+#endif
+
 namespace rasr_gmm {
 namespace dev {
 
@@ -431,6 +435,13 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         best[cb][r] = min(best[cb][r], min(pack(accA[cb][r], P0[r]), pack(accB[cb][r], P1[r])));
+#if GMM_I8_INTERLEAVE
+#pragma unroll
+                for (int i = 0; i < 2 * NF * KS; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, GMM_I8_INTERLEAVE, 0);  // VALU
+                }
+#endif
                 t += 2;
             }
             else {
