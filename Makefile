@@ -16,15 +16,18 @@ SPLITFLAGS = -mllvm -amdgpu-mfma-vgpr-form
 HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc
-HDRS      = include/rasr_gmm.h $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh \
+HDRS      = include/rasr_gmm.h $(SRC)/gmm_presel.hh $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh \
             $(SRC)/host/GpuFeatureScorer.hh include/rasr_gmm_io.h include/rasr_nn.h $(SRC)/nn_kernels.hh
 
 LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
-            $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o
+            $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
+            $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
-all: $(LIB) $(DRIVER) oracle
+REFSORT   = $(BUILD)/tests/refsort_test
+
+all: $(LIB) $(DRIVER) $(REFSORT) oracle
 
 $(BUILD)/gmm_kernels_i8.o: $(SRC)/gmm_kernels_i8.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -37,6 +40,15 @@ $(BUILD)/gmm_kernels_f32.o: $(SRC)/gmm_kernels_f32.hip $(HDRS)
 $(BUILD)/gmm_kernels_split.o: $(SRC)/gmm_kernels_split.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(SPLITFLAGS) -c $< -o $@
+
+# density preselection: clustering assignment + per-frame cluster selection (std::sort replay)
+$(BUILD)/gmm_kernels_presel.o: $(SRC)/gmm_kernels_presel.hip $(SRC)/gmm_refsort.hh $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/gmm_presel.o: $(SRC)/gmm_presel.cc $(SRC)/gmm_presel.hh $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
 # hybrid-DNN scorer (include/rasr_nn.h): bf16 MFMA GEMM per layer
 $(BUILD)/nn_kernels.o: $(SRC)/nn_kernels.hip $(HDRS)
@@ -66,6 +78,11 @@ $(BUILD)/MixtureSetFile.o: $(SRC)/host/MixtureSetFile.cc $(HDRS)
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz
+
+# host pin of the GPU std::sort replay (gmm_refsort.hh) against this image's std::sort
+$(REFSORT): tests/cpp/refsort_test.cc $(SRC)/gmm_refsort.hh
+	@mkdir -p $(BUILD)/tests
+	g++ -std=c++17 -O2 -Wall -o $@ $<
 
 $(DRIVER): tests/cpp/feature_scorer_driver.cc $(LIB) $(HDRS)
 	@mkdir -p $(BUILD)/tests

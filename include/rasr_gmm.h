@@ -34,6 +34,8 @@ extern "C" {
  * (src/Mm/Module.cc:84-107). */
 typedef enum {
     GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT = 0, /* "batch-diagonal-maximum-float" BatchFeatureScorer.cc:120-234 */
+    GMM_BATCH_PRESELECTION_FLOAT     = 1, /* "preselection-batch-float"     BatchFeatureScorer.cc:238-289 */
+    GMM_BATCH_PRESELECTION_INT       = 2, /* "preselection-batch-int"       BatchFeatureScorer.cc:478-533 */
     GMM_BATCH_DIAGONAL_MAXIMUM_INT   = 3, /* "batch-diagonal-maximum-int"   BatchFeatureScorer.cc:293-474 */
     GMM_BATCH_DIAGONAL_MAXIMUM_FAST  = 4, /* "batch-diagonal-maximum-fast"  BatchFeatureScorer.cc:537-604 */
     GMM_DIAGONAL_MAXIMUM             = 5, /* "diagonal-maximum"   GaussDiagonalMaximumFeatureScorer.cc */
@@ -72,6 +74,12 @@ typedef struct {
     uint32_t mixture_begin;        /* mixture shard [begin, end) scored by this handle; 0,0 = all mixtures        */
     uint32_t mixture_end;
     uint32_t flags;                /* GMM_FLAG_* bits, 0 = defaults                                               */
+    /* density preselection (preselection-batch-*): the "density-clustering" parameters,
+     * DensityClustering.cc:19-32.  The clustering is built at create time (no cache-archive). */
+    uint32_t clusters;              /* "clusters" (256, range 1..256), reduced to the density count      */
+    uint32_t select_clusters;       /* "select-clusters" (32)                                           */
+    uint32_t clustering_iterations; /* "iterations" (5)                                                 */
+    float    backoff_score;         /* "backoff-score" (40000): float type, mixture with no selected density */
 } gmm_scorer_config;
 
 /* Float types (diagonal-maximum, batch-float) with one covariance run on the f16
@@ -149,6 +157,20 @@ int gmm_scorer_launch_info(const gmm_scorer* scorer, uint32_t n_frames, uint32_t
  * the summed kernel time and launch count since the last reset. */
 int gmm_scorer_set_timing(gmm_scorer* scorer, int enable);
 int gmm_scorer_kernel_time(gmm_scorer* scorer, double* total_ms, uint32_t* n_launches, int reset);
+
+/* Density preselection (preselection-batch-float / -int).
+ * gmm_scorer_density_clustering: the clustering the handle was built with, over ALL mixture entries of
+ * the mixture set (entry = CSR position in mixture_densities, the reference's density index):
+ *   cluster_of_entry [n_entries] (clusterIndexForDensity_), cluster_means [clusters][padded_dimension]
+ *   (f32 for the float type, u8 for the int type; padded dimension = dimension rounded up to 8 / 16).
+ * gmm_scorer_cluster_selection: the selection the last gmm_score_* call used, [n_frames][clusters]
+ *   0/1 (activeClusters_); synchronizes the device.
+ * gmm_density_clustering_seeds: host-only, the entry each cluster is initialized from
+ *   (initializeClusters: srand(1), rand() % n_entries without repetition, DensityClustering.tcc:60-74). */
+int gmm_scorer_density_clustering(const gmm_scorer* scorer, uint32_t* n_clusters, uint32_t* padded_dimension,
+                                  uint8_t* cluster_of_entry, void* cluster_means);
+int gmm_scorer_cluster_selection(gmm_scorer* scorer, uint32_t n_frames, uint8_t* selection);
+int gmm_density_clustering_seeds(uint32_t n_entries, uint32_t n_clusters, uint32_t* seed_entries);
 
 const char* gmm_last_error(void);
 const char* gmm_version(void);

@@ -539,6 +539,10 @@ typedef struct {
     const float*   frames;
     uint32_t       n_frames, frame_stride;
     float*         scores;
+    /* preselection-batch-int (ClusterIterator, BatchFeatureScorer.cc:500-529): NULL = every density */
+    const uint8_t* entry_cluster;  /* clusterIndexForDensity_ [entries]              */
+    const uint8_t* selection;      /* activeClusters_ [n_frames][n_clusters]          */
+    uint32_t       n_clusters;
 } orc_bint_ctx;
 
 static void orc_bint_frames(void* p, uint32_t t0, uint32_t t1) {
@@ -555,6 +559,8 @@ static void orc_bint_frames(void* p, uint32_t t0, uint32_t t1) {
             /* fillScoreCacheTpl -- cc:423-470 */
             int32_t best = 2147483647;
             for (i = x->ms->mixture_offsets[e]; i < x->ms->mixture_offsets[e + 1]; ++i) {
+                if (x->selection && !x->selection[(size_t)t * x->n_clusters + x->entry_cluster[i]])
+                    continue; /* selector.value() false -- cc:439 */
                 int32_t tmp = orc_l2norm_u8(x->means + (size_t)i * x->Dp, feature, x->Dp);
                 tmp += x->constants[i];
                 if (tmp < best)
@@ -568,6 +574,12 @@ static void orc_bint_frames(void* p, uint32_t t0, uint32_t t1) {
 
 int orc_batch_int_score(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
                         uint32_t frame_stride, float* scores, int n_threads) {
+    return orc_batch_int_score_sel(ms, frames, n_frames, frame_stride, scores, n_threads, NULL, NULL, 0);
+}
+
+int orc_batch_int_score_sel(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
+                            uint32_t frame_stride, float* scores, int n_threads, const uint8_t* entry_cluster,
+                            const uint8_t* selection, uint32_t n_clusters) {
     orc_bint_ctx x;
     uint32_t     k, i, m, D = ms->dimension;
     float        isv0[4096];
@@ -620,6 +632,9 @@ int orc_batch_int_score(const orc_mixture_set* ms, const float* frames, uint32_t
     x.n_frames = n_frames;
     x.frame_stride = frame_stride;
     x.scores = scores;
+    x.entry_cluster = entry_cluster;
+    x.selection = selection;
+    x.n_clusters = n_clusters;
     orc_parallel_frames(orc_bint_frames, &x, n_frames, n_threads);
     free(x.variance);
     free(x.means);
@@ -639,6 +654,11 @@ typedef struct {
     const float* frames;
     uint32_t n_frames, frame_stride;
     float*   scores;
+    /* preselection-batch-float (ClusterDensitySelection, BatchFeatureScorer.cc:265-289): NULL = all */
+    const uint8_t* entry_cluster;
+    const uint8_t* selection;
+    uint32_t n_clusters;
+    float    backoff;
 } orc_bflt_ctx;
 
 static void orc_bflt_frames(void* p, uint32_t t0, uint32_t t1) {
@@ -655,6 +675,8 @@ static void orc_bflt_frames(void* p, uint32_t t0, uint32_t t1) {
             /* fillScoreCacheTpl -- cc:187-234 */
             float score = FLT_MAX;
             for (i = x->ms->mixture_offsets[e]; i < x->ms->mixture_offsets[e + 1]; ++i) {
+                if (x->selection && !x->selection[(size_t)t * x->n_clusters + x->entry_cluster[i]])
+                    continue; /* if (!selector(rp, dns)) continue; -- cc:206-207 */
                 const float* mean = x->means + (size_t)i * x->Dp;
                 v4sf s1 = {x->constants[i], 0, 0, 0}, s2 = {0, 0, 0, 0}, a, b, x1, x2, r;
                 uint32_t d;
@@ -678,6 +700,8 @@ static void orc_bflt_frames(void* p, uint32_t t0, uint32_t t1) {
             }
             if (score < FLT_MAX)
                 score *= 0.5;
+            if (x->selection && score == FLT_MAX)
+                score = x->backoff; /* BatchPreselectionFloatFeatureScorer::fillScoreCache, cc:282-288 */
             x->scores[(size_t)e * x->n_frames + t] = score;
         }
     }
@@ -686,6 +710,12 @@ static void orc_bflt_frames(void* p, uint32_t t0, uint32_t t1) {
 
 int orc_batch_float_score(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
                           uint32_t frame_stride, float* scores, int n_threads) {
+    return orc_batch_float_score_sel(ms, frames, n_frames, frame_stride, scores, n_threads, NULL, NULL, 0, 0.0f);
+}
+
+int orc_batch_float_score_sel(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
+                              uint32_t frame_stride, float* scores, int n_threads, const uint8_t* entry_cluster,
+                              const uint8_t* selection, uint32_t n_clusters, float backoff) {
     orc_bflt_ctx x;
     uint32_t     k, m, D = ms->dimension;
     float        logNormFactor;
@@ -718,6 +748,10 @@ int orc_batch_float_score(const orc_mixture_set* ms, const float* frames, uint32
     x.n_frames = n_frames;
     x.frame_stride = frame_stride;
     x.scores = scores;
+    x.entry_cluster = entry_cluster;
+    x.selection = selection;
+    x.n_clusters = n_clusters;
+    x.backoff = backoff;
     orc_parallel_frames(orc_bflt_frames, &x, n_frames, n_threads);
     free(x.variance);
     free(x.means);
@@ -766,5 +800,53 @@ int orc_batch_int_prepare(const orc_mixture_set* ms, float* scale_out, float* va
     *scale_out = scale_;
     memcpy(variance_out, variance, sizeof(float) * D);
     free(variance);
+    return 0;
+}
+
+/* BatchFloatFeatureScorer::init / setFeature tables (BatchFeatureScorer.cc:144-170, 137-142):
+ *   variance [Dp] (isv, 0-padded), means [entries][Dp] = mean * variance (f32), constants [entries] */
+int orc_batch_float_tables(const orc_mixture_set* ms, float* variance_out, float* means_out, float* constants_out) {
+    uint32_t k, m, D = ms->dimension, Dp = (ms->dimension + 7u) / 8u * 8u;
+    float    logNormFactor;
+    if (ms->n_covariances != 1)
+        return -1;
+    memset(variance_out, 0, sizeof(float) * Dp);
+    for (k = 0; k < D; ++k)
+        variance_out[k] = orc_inverse_sqrt(ms->variances[k]);
+    logNormFactor = (float)orc_gauss_log_norm(ms->variances, D);
+    memset(means_out, 0, sizeof(float) * (size_t)ms->mixture_offsets[ms->n_mixtures] * Dp);
+    for (m = 0; m < ms->n_mixtures; ++m) {
+        uint32_t e;
+        for (e = ms->mixture_offsets[m]; e < ms->mixture_offsets[m + 1]; ++e) {
+            const float* mean = ms->means + (size_t)ms->density_mean[ms->mixture_densities[e]] * D;
+            for (k = 0; k < D; ++k)
+                means_out[(size_t)e * Dp + k] = mean[k] * variance_out[k];
+            constants_out[e] = logNormFactor - 2 * ms->mixture_log_weights[e];
+        }
+    }
+    return 0;
+}
+
+/* BatchIntFeatureScorer::init / setFeature tables (BatchFeatureScorer.cc:339-390):
+ *   variance [Dp] (isv * scale, 0-padded), means [entries][Dp] u8 (quantize(mean * variance)) */
+int orc_batch_int_tables(const orc_mixture_set* ms, float* variance_out, uint8_t* means_out) {
+    uint32_t k, m, D = ms->dimension, Dp = (ms->dimension + 15u) / 16u * 16u;
+    float    scale_;
+    int32_t* constants = (int32_t*)malloc(sizeof(int32_t) * (ms->mixture_offsets[ms->n_mixtures] + 1));
+    memset(variance_out, 0, sizeof(float) * Dp);
+    if (orc_batch_int_prepare(ms, &scale_, variance_out, constants) != 0) {
+        free(constants);
+        return -1;
+    }
+    free(constants);
+    memset(means_out, 0, (size_t)ms->mixture_offsets[ms->n_mixtures] * Dp);
+    for (m = 0; m < ms->n_mixtures; ++m) {
+        uint32_t e;
+        for (e = ms->mixture_offsets[m]; e < ms->mixture_offsets[m + 1]; ++e) {
+            const float* mean = ms->means + (size_t)ms->density_mean[ms->mixture_densities[e]] * D;
+            for (k = 0; k < D; ++k)
+                means_out[(size_t)e * Dp + k] = orc_quantize(mean[k] * variance_out[k]);
+        }
+    }
     return 0;
 }

@@ -108,6 +108,19 @@ int orc_batch_int_score(const orc_mixture_set* ms, const float* frames, uint32_t
 int orc_batch_float_score(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
                           uint32_t frame_stride, float* scores, int n_threads);
 
+/* ---- preselection-batch-int / -float (BatchFeatureScorer.cc:238-289, 478-533): the batch scorers
+ * restricted to the densities whose cluster the frame selected; entry_cluster [entries] is
+ * clusterIndexForDensity_, selection [n_frames][n_clusters] activeClusters_ (presel_oracle.cc) ---- */
+int orc_batch_int_score_sel(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
+                            uint32_t frame_stride, float* scores, int n_threads, const uint8_t* entry_cluster,
+                            const uint8_t* selection, uint32_t n_clusters);
+int orc_batch_float_score_sel(const orc_mixture_set* ms, const float* frames, uint32_t n_frames,
+                              uint32_t frame_stride, float* scores, int n_threads, const uint8_t* entry_cluster,
+                              const uint8_t* selection, uint32_t n_clusters, float backoff);
+/* the prepared tables the clustering runs on: Dp = dimension padded to 8 (float) / 16 (int) */
+int orc_batch_float_tables(const orc_mixture_set* ms, float* variance_out, float* means_out, float* constants_out);
+int orc_batch_int_tables(const orc_mixture_set* ms, float* variance_out, uint8_t* means_out);
+
 /* ---- helpers for known-answer tests ---- */
 void orc_quantize_array(const float* x, uint32_t n, uint8_t* out);
 int  orc_batch_int_prepare(const orc_mixture_set* ms, float* scale_out, float* variance_out, int32_t* constants_out);

@@ -84,6 +84,13 @@ def load() -> ctypes.CDLL:
                                                ctypes.c_uint32, _vp, ctypes.c_int]),
         "orc_batch_float_score": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, ctypes.c_uint32,
                                                  ctypes.c_uint32, _vp, ctypes.c_int]),
+        "orc_batch_int_score_sel": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, ctypes.c_uint32,
+                                                   ctypes.c_uint32, _vp, ctypes.c_int, _vp, _vp, ctypes.c_uint32]),
+        "orc_batch_float_score_sel": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, ctypes.c_uint32,
+                                                     ctypes.c_uint32, _vp, ctypes.c_int, _vp, _vp, ctypes.c_uint32,
+                                                     ctypes.c_float]),
+        "orc_batch_float_tables": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, _vp, _vp]),
+        "orc_batch_int_tables": (ctypes.c_int, [ctypes.POINTER(OrcMixtureSet), _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -283,3 +290,124 @@ def batch_int_prepare(ms):
                                     const.ctypes.data_as(_vp)) != 0:
         raise ValueError("orc_batch_int_prepare failed")
     return scale.value, var, const
+
+
+# ---------------------------------------------------------------------------
+# preselection-batch-float / -int (oracle/presel_oracle.cc + the batch scorers with a selector)
+# ---------------------------------------------------------------------------
+PRESEL_LIB = os.path.join(_HERE, "_build", "libpresel_oracle.so")
+_presel = None
+
+
+def load_presel() -> ctypes.CDLL:
+    global _presel
+    if _presel is not None:
+        return _presel
+    if not os.path.exists(PRESEL_LIB):
+        build()
+    lib = ctypes.CDLL(PRESEL_LIB)
+    u32 = ctypes.c_uint32
+    for name, args in {
+        "orc_libc_rand_sequence": [u32, u32, _vp],
+        "orc_cluster_build_f32": [_vp, u32, u32, u32, u32, _vp, _vp],
+        "orc_cluster_build_u8": [_vp, u32, u32, u32, u32, _vp, _vp],
+        "orc_select_clusters_f32": [_vp, u32, _vp, u32, u32, u32, _vp],
+        "orc_select_clusters_u8": [_vp, u32, _vp, u32, u32, u32, _vp],
+    }.items():
+        f = getattr(lib, name)
+        f.restype = ctypes.c_int
+        f.argtypes = args
+    _presel = lib
+    return lib
+
+
+def libc_rand_sequence(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, np.int32)
+    load_presel().orc_libc_rand_sequence(seed, n, out.ctypes.data_as(_vp))
+    return out
+
+
+class OraclePresel:
+    """preselection-batch-float (kind "float") / preselection-batch-int (kind "int") restated:
+    DensityClustering over the batch scorer's prepared means, per-frame selection of the n_select
+    nearest clusters, the batch scorer over the selected densities (backoff score for a float
+    mixture without any, BatchFeatureScorer.cc:282-288)."""
+
+    def __init__(self, ms, kind: str, clusters: int = 256, select: int = 32, iterations: int = 5,
+                 backoff: float = 40000.0):
+        assert kind in ("float", "int")
+        self.kind = kind
+        self.ms = ms
+        self._d = _Desc(ms)
+        lib = load()
+        D = int(self._d.c.dimension)
+        E = self._d.n_entries
+        if kind == "float":
+            self.dp = (D + 7) // 8 * 8
+            self.variance = np.zeros(self.dp, np.float32)
+            self.means = np.zeros((E, self.dp), np.float32)
+            consts = np.zeros(E, np.float32)
+            rc = lib.orc_batch_float_tables(ctypes.byref(self._d.c), self.variance.ctypes.data_as(_vp),
+                                            self.means.ctypes.data_as(_vp), consts.ctypes.data_as(_vp))
+        else:
+            self.dp = (D + 15) // 16 * 16
+            self.variance = np.zeros(self.dp, np.float32)
+            self.means = np.zeros((E, self.dp), np.uint8)
+            rc = lib.orc_batch_int_tables(ctypes.byref(self._d.c), self.variance.ctypes.data_as(_vp),
+                                          self.means.ctypes.data_as(_vp))
+        if rc != 0:
+            raise ValueError("batch tables failed")
+        # DensityClusteringBase::init (DensityClustering.cc:48-61)
+        self.n_clusters = min(int(clusters), E)
+        self.n_select = int(select)
+        if self.n_select > self.n_clusters:
+            raise ValueError("select-clusters exceeds the number of clusters")
+        self.backoff = float(backoff)
+        self.cluster_of_entry = np.zeros(E, np.uint8)
+        self.cluster_means = np.zeros((self.n_clusters, self.dp), self.means.dtype)
+        fn = load_presel().orc_cluster_build_f32 if kind == "float" else load_presel().orc_cluster_build_u8
+        if fn(self.means.ctypes.data_as(_vp), E, self.dp, self.n_clusters, int(iterations),
+              self.cluster_of_entry.ctypes.data_as(_vp), self.cluster_means.ctypes.data_as(_vp)) != 0:
+            raise ValueError("cluster build failed")
+
+    def features(self, frames):
+        """setFeature (BatchFeatureScorer.cc:137-142 / 382-388): [n][Dp]"""
+        f, n, _ = _frames(frames)
+        D = int(self._d.c.dimension)
+        x = f[:, :D] * self.variance[None, :D]
+        if self.kind == "float":
+            out = np.zeros((n, self.dp), np.float32)
+            out[:, :D] = x
+            return out
+        out = np.zeros((n, self.dp), np.uint8)
+        out[:, :D] = quantize_array(x).reshape(n, D)
+        return out
+
+    def select(self, frames) -> np.ndarray:
+        """activeClusters_ per frame: [n][n_clusters] 0/1 (DensityClustering.tcc:151-176)"""
+        feats = np.ascontiguousarray(self.features(frames))
+        n = feats.shape[0]
+        sel = np.zeros((n, self.n_clusters), np.uint8)
+        fn = load_presel().orc_select_clusters_f32 if self.kind == "float" else load_presel().orc_select_clusters_u8
+        fn(feats.ctypes.data_as(_vp), n, self.cluster_means.ctypes.data_as(_vp), self.n_clusters, self.dp,
+           self.n_select, sel.ctypes.data_as(_vp))
+        return sel
+
+    def score(self, frames, n_threads: int = 1, selection=None):
+        f, n, stride = _frames(frames)
+        sel = np.ascontiguousarray(self.select(f) if selection is None else selection, dtype=np.uint8)
+        scores = np.empty((self._d.n_mixtures, n), np.float32)
+        lib = load()
+        if self.kind == "float":
+            rc = lib.orc_batch_float_score_sel(ctypes.byref(self._d.c), f.ctypes.data_as(_vp), n, stride,
+                                               scores.ctypes.data_as(_vp), int(n_threads),
+                                               self.cluster_of_entry.ctypes.data_as(_vp), sel.ctypes.data_as(_vp),
+                                               self.n_clusters, self.backoff)
+        else:
+            rc = lib.orc_batch_int_score_sel(ctypes.byref(self._d.c), f.ctypes.data_as(_vp), n, stride,
+                                             scores.ctypes.data_as(_vp), int(n_threads),
+                                             self.cluster_of_entry.ctypes.data_as(_vp), sel.ctypes.data_as(_vp),
+                                             self.n_clusters)
+        if rc != 0:
+            raise ValueError("preselection score failed")
+        return scores

@@ -20,6 +20,8 @@ GMM_FLAG_SPLIT_TILE32 = 4
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0
+BATCH_PRESELECTION_FLOAT = 1
+BATCH_PRESELECTION_INT = 2
 BATCH_DIAGONAL_MAXIMUM_INT = 3
 BATCH_DIAGONAL_MAXIMUM_FAST = 4
 DIAGONAL_MAXIMUM = 5
@@ -30,6 +32,8 @@ SCORER_TYPES = {
     "batch-diagonal-maximum-float": BATCH_DIAGONAL_MAXIMUM_FLOAT,
     "batch-diagonal-maximum-int": BATCH_DIAGONAL_MAXIMUM_INT,
     "batch-diagonal-maximum-fast": BATCH_DIAGONAL_MAXIMUM_FAST,
+    "preselection-batch-float": BATCH_PRESELECTION_FLOAT,
+    "preselection-batch-int": BATCH_PRESELECTION_INT,
     "diagonal-maximum": DIAGONAL_MAXIMUM,
     "SIMD-diagonal-maximum": SIMD_DIAGONAL_MAXIMUM,
     "diagonal-sum": DIAGONAL_SUM,
@@ -66,6 +70,10 @@ class ScorerConfig(ctypes.Structure):
         ("mixture_begin", ctypes.c_uint32),
         ("mixture_end", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
+        ("clusters", ctypes.c_uint32),
+        ("select_clusters", ctypes.c_uint32),
+        ("clustering_iterations", ctypes.c_uint32),
+        ("backoff_score", ctypes.c_float),
     ]
 
 
@@ -96,6 +104,10 @@ PROTOTYPES = [
     ("gmm_scorer_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("gmm_scorer_kernel_time", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), _u32p, ctypes.c_int]),
+    ("gmm_scorer_density_clustering", ctypes.c_int,
+     [ctypes.c_void_p, _u32p, _u32p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("gmm_scorer_cluster_selection", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("gmm_density_clustering_seeds", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, _u32p]),
     ("gmm_last_error", ctypes.c_char_p, []),
     # include/rasr_gmm_io.h
     ("gmm_mixture_set_read", ctypes.c_int,

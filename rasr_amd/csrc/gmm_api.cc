@@ -19,6 +19,7 @@
 #include "../../include/rasr_gmm.h"
 #include "gmm_kernels.hh"
 #include "gmm_prepare.hh"
+#include "gmm_presel.hh"
 
 using namespace rasr_gmm;
 
@@ -81,6 +82,13 @@ struct gmm_scorer {
     uint32_t          splitRows  = 16;     // split kernel tile height
     uint32_t          tileBits   = 1;
     float             offsetK0   = 0;
+    // density preselection (preselection-batch-*)
+    bool                    presel = false;
+    DensityClustering       clustering;
+    void*                   dClusterMeans = nullptr;
+    uint32_t*               dSelT         = nullptr;  // [nFramesPad/64][clusters][16]
+    uint16_t*               dTileClu      = nullptr;  // [tiles + pad][16] cluster * 64
+    uint32_t                lastFrames    = 0;
     // quantized scalars
     uint32_t idxBits = 1, paddedDimension = 0;
     float    scaling = 0, scalingSquared = 0, invQ = 0, batchScale = 0;
@@ -115,7 +123,7 @@ struct gmm_scorer {
     ~gmm_scorer() {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
                         dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
-                        dFrameExp, dDimScale, dLimbExp};
+                        dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu};
         for (void* p : ptrs)
             if (p)
                 (void)hipFree(p);
@@ -132,7 +140,19 @@ struct gmm_scorer {
 namespace {
 
 uint32_t framesPerBlock(const gmm_scorer* s) {
-    return s->quantized ? kI8FramesPerBlock : (s->split ? kSplitFramesPerBlock : kF32FramesPerBlock);
+    if (s->quantized)
+        return s->presel ? kI8PreselFramesPerBlock : kI8FramesPerBlock;
+    return s->split ? kSplitFramesPerBlock : kF32FramesPerBlock;
+}
+
+// the selection of every frame of the call: mask words for whole 64-frame blocks (padding frames too)
+int selectClustersFor(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nPadCall,
+                      hipStream_t stream) {
+    GMM_HIP_CHECK(launchSelectClusters(s->quantized, frames, nFrames, frameStride, nPadCall, s->D,
+                                       s->clustering.paddedDimension, s->dIsv, s->dClusterMeans,
+                                       s->clustering.nClusters, s->clustering.nSelected, s->dSelT, stream));
+    s->lastFrames = nFrames;
+    return GMM_OK;
 }
 
 // Cut the shard's mixtures into chunks of about equal tile count so that
@@ -213,6 +233,8 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
     int               rc       = chunkTableFor(s, nFrameTiles, &ct);
     if (rc != GMM_OK)
         return rc;
+    if (s->presel && (rc = selectClustersFor(s, frames, nFrames, frameStride, nPadCall, stream)) != GMM_OK)
+        return rc;
     if (s->quantized) {
         GMM_HIP_CHECK(launchPrepareFramesI8(frames, nFrames, frameStride, s->nFramesPad, nPadCall, s->D, s->C,
                                             s->kSteps, s->dIsv, s->dFrameQ, s->dFrameSS, stream));
@@ -237,6 +259,10 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.s2          = s->scalingSquared;
         a.batchScale  = s->batchScale;
         a.outScale    = s->cfg.score_scale;
+        a.presel      = s->presel ? 1 : 0;
+        a.selT        = s->dSelT;
+        a.tileClu     = s->dTileClu;
+        a.nClusters   = s->clustering.nClusters;
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         GMM_HIP_CHECK(launchScoreI8(a, s->kSteps, s->multiCov, stream));
@@ -265,6 +291,11 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.tileBits    = s->tileBits;
         a.offsetK0    = s->offsetK0;
         a.outScale    = s->cfg.score_scale;
+        a.presel      = s->presel ? 1 : 0;
+        a.selT        = s->dSelT;
+        a.tileClu     = s->dTileClu;
+        a.nClusters   = s->clustering.nClusters;
+        a.backoff     = s->cfg.backoff_score;
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         if (s->flavor == Flavor::DiagonalSum)
@@ -312,6 +343,8 @@ Flavor flavorOf(gmm_scorer_type t, bool* quantized, bool* ok) {
         case GMM_BATCH_DIAGONAL_MAXIMUM_FAST: *quantized = true; return Flavor::BatchInt;
         case GMM_DIAGONAL_MAXIMUM: *quantized = false; return Flavor::DiagonalMaximum;
         case GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT: *quantized = false; return Flavor::BatchFloat;
+        case GMM_BATCH_PRESELECTION_FLOAT: *quantized = false; return Flavor::BatchFloat;
+        case GMM_BATCH_PRESELECTION_INT: *quantized = true; return Flavor::BatchInt;
         case GMM_DIAGONAL_SUM: *quantized = false; return Flavor::DiagonalSum;
     }
     *ok = false;
@@ -330,7 +363,55 @@ void gmm_default_config(gmm_scorer_config* cfg) {
     cfg->gaussian_scale       = 1.0f;
     cfg->score_scale          = 1.0f;
     cfg->max_frames           = 4;  // "buffer-size" default, BatchFeatureScorer.cc:28-29
+    cfg->clusters              = 256;  // DensityClustering.cc:19-32
+    cfg->select_clusters       = 32;
+    cfg->clustering_iterations = 5;
+    cfg->backoff_score         = 40000.0f;
 }
+
+}  // extern "C"
+
+namespace {
+
+// preselection: the clustering over all entries' prepared means, the tiles' row cluster offsets and the
+// per-call mask table.  rowEntry / fill: the scorer tiling (16 rows) and, for the split layout, the
+// entry a padding row repeats (a padding row must be deselected with the row it copies).
+int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entryMeans, uint32_t Dp,
+                      const std::vector<uint32_t>& rowEntry, const std::vector<uint32_t>* fill) {
+    const uint32_t nEntries = ms.mixture_offsets[ms.n_mixtures];
+    std::string    err = buildDensityClustering(s->quantized, entryMeans, nEntries, Dp, s->cfg.clusters,
+                                                s->cfg.select_clusters, s->cfg.clustering_iterations, s->clustering);
+    if (!err.empty())
+        return fail(GMM_ERR_INVALID_ARGUMENT, err);
+    const DensityClustering& dc = s->clustering;
+    const uint32_t           T  = static_cast<uint32_t>(rowEntry.size() / kTileRows);
+    std::vector<uint16_t>    clu(static_cast<size_t>(T + kTilePad) * kTileRows, 0);
+    for (uint32_t t = 0; t < T; ++t)
+        for (uint32_t r = 0; r < kTileRows; ++r) {
+            uint32_t e = rowEntry[static_cast<size_t>(t) * kTileRows + r];
+            if (e == UINT32_MAX && fill)
+                e = (*fill)[t];
+            const uint32_t c = e == UINT32_MAX ? 0u : dc.clusterOfEntry[e];
+            clu[static_cast<size_t>(t) * kTileRows + r] = static_cast<uint16_t>(c * 64u);
+        }
+    int rc = upload(&s->dTileClu, clu);
+    if (rc != GMM_OK)
+        return rc;
+    if (s->quantized)
+        rc = upload(reinterpret_cast<uint8_t**>(&s->dClusterMeans), dc.meansQ);
+    else
+        rc = upload(reinterpret_cast<float**>(&s->dClusterMeans), dc.meansF);
+    if (rc != GMM_OK)
+        return rc;
+    const size_t selBytes = static_cast<size_t>(s->nFramesPad / 64) * dc.nClusters * 64;
+    GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dSelT), selBytes));
+    GMM_HIP_CHECK(hipMemset(s->dSelT, 0xff, selBytes));
+    return GMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scorer_config* config,
                       int device, gmm_scorer** out) {
@@ -349,6 +430,11 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         return fail(GMM_ERR_INVALID_ARGUMENT, "max_frames must be > 0");
     if (type == GMM_BATCH_DIAGONAL_MAXIMUM_FAST && (ms->dimension + 15) / 16 * 16 > 48)
         return fail(GMM_ERR_UNSUPPORTED, "This feature scorer supports only features with max. 48 components");
+    const bool presel = type == GMM_BATCH_PRESELECTION_FLOAT || type == GMM_BATCH_PRESELECTION_INT;
+    if (presel && (cfg.clusters == 0 || cfg.clusters > 256))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "clusters must be in [1, 256]");
+    if (presel && (cfg.flags & (GMM_FLAG_NATIVE_F32 | GMM_FLAG_SPLIT_TILE32)))
+        return fail(GMM_ERR_UNSUPPORTED, "preselection runs on the 16-row split-f16 / quantized kernels only");
     ShardRange shard{cfg.mixture_begin, cfg.mixture_end};
 
     auto s      = std::make_unique<gmm_scorer>();
@@ -360,6 +446,7 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     s->D        = ms->dimension;
     s->C        = ms->n_covariances;
     s->nFramesPad = (cfg.max_frames + kFramePadQuantum - 1) / kFramePadQuantum * kFramePadQuantum;
+    s->presel     = presel;
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -401,15 +488,23 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameSS), nQ * sizeof(int32_t)));
         GMM_HIP_CHECK(hipMemset(s->dFrameSS, 0, nQ * sizeof(int32_t)));
         (void)tiling;
+        // BatchPreselectionIntFeatureScorer::init: clustering_->build(means_) over the u8 means
+        if (presel && (rc = setupPreselection(s.get(), *ms, p.preparedMean.data(), p.paddedDimension,
+                                              p.tiling.rowEntry, nullptr)) != GMM_OK)
+            return rc;
     }
     else {
         PreparedFloat p;
         std::string   err = prepareFloat(*ms, flavor, cfg.mixture_weight_scale, cfg.gaussian_scale, shard, p,
                                          (cfg.flags & GMM_FLAG_NATIVE_F32) == 0,
-                                         (cfg.flags & GMM_FLAG_SPLIT_TILE16) ? 16u
-                                                                              : ((cfg.flags & GMM_FLAG_SPLIT_TILE32) ? 32u : 0u));
+                                         (presel || (cfg.flags & GMM_FLAG_SPLIT_TILE16))
+                                                 ? 16u
+                                                 : ((cfg.flags & GMM_FLAG_SPLIT_TILE32) ? 32u : 0u));
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
+        if (presel && (!p.split || p.splitRows != 16))
+            return fail(GMM_ERR_UNSUPPORTED, "preselection-batch-float needs the 16-row split-f16 layout (one "
+                                             "covariance, dimension <= 83, <= 1024 densities per mixture)");
         s->split    = p.split;
         s->kSteps16 = p.kSteps16;
         s->splitRows = p.splitRows;
@@ -434,6 +529,20 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
             GMM_HIP_CHECK(hipMemset(s->dFrameXX, 0, s->nFramesPad * sizeof(float)));
             GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameExp), s->nFramesPad * sizeof(int32_t)));
             GMM_HIP_CHECK(hipMemset(s->dFrameExp, 0, s->nFramesPad * sizeof(int32_t)));
+            if (presel) {
+                // BatchPreselectionFloatFeatureScorer::init: clustering over means_ = mean * isv (f32),
+                // 0-padded to the batch-float padded dimension (BlockSize 8, BatchFeatureScorer.cc:145-170)
+                const uint32_t     D = ms->dimension, Dp = (D + 7u) / 8u * 8u;
+                const uint32_t     nEntries = ms->mixture_offsets[ms->n_mixtures];
+                std::vector<float> em(static_cast<size_t>(nEntries) * Dp, 0.0f);
+                for (uint32_t e = 0; e < nEntries; ++e) {
+                    const float* mean = ms->means + static_cast<size_t>(ms->density_mean[ms->mixture_densities[e]]) * D;
+                    for (uint32_t k = 0; k < D; ++k)
+                        em[static_cast<size_t>(e) * Dp + k] = mean[k] * p.isv[k];
+                }
+                if ((rc = setupPreselection(s.get(), *ms, em.data(), Dp, p.tiling.rowEntry, &p.splitFillEntry)) != GMM_OK)
+                    return rc;
+            }
             s->mixBase = shard.begin == 0 && shard.end == 0 ? 0 : shard.begin;
             GMM_HIP_CHECK(hipDeviceSynchronize());
             *out = s.release();
@@ -578,7 +687,7 @@ int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLau
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
     (void)nFrames;
     if (nLaunches)
-        *nLaunches = 2;
+        *nLaunches = s->presel ? 3 : 2;
     if (name)
         *name = s->quantized ? "scoreI8" : (s->split ? (s->flavor == Flavor::DiagonalSum ? "scoreSplitSum"
                                                                          : (s->splitRows == 32 ? "scoreSplit32" : "scoreSplit"))
@@ -611,6 +720,58 @@ int gmm_scorer_kernel_time(gmm_scorer* s, double* totalMs, uint32_t* nLaunches, 
         *nLaunches = static_cast<uint32_t>(s->eventsUsed);
     if (reset)
         s->eventsUsed = 0;
+    return GMM_OK;
+}
+
+int gmm_scorer_density_clustering(const gmm_scorer* s, uint32_t* nClusters, uint32_t* paddedDimension,
+                                  uint8_t* clusterOfEntry, void* clusterMeans) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    if (!s->presel)
+        return fail(GMM_ERR_UNSUPPORTED, "scorer type has no density preselection");
+    const DensityClustering& dc = s->clustering;
+    if (nClusters)
+        *nClusters = dc.nClusters;
+    if (paddedDimension)
+        *paddedDimension = dc.paddedDimension;
+    if (clusterOfEntry)
+        std::copy(dc.clusterOfEntry.begin(), dc.clusterOfEntry.end(), clusterOfEntry);
+    if (clusterMeans) {
+        if (dc.quantized)
+            std::copy(dc.meansQ.begin(), dc.meansQ.end(), static_cast<uint8_t*>(clusterMeans));
+        else
+            std::copy(dc.meansF.begin(), dc.meansF.end(), static_cast<float*>(clusterMeans));
+    }
+    return GMM_OK;
+}
+
+int gmm_scorer_cluster_selection(gmm_scorer* s, uint32_t nFrames, uint8_t* selection) {
+    if (!s || !selection)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    if (!s->presel)
+        return fail(GMM_ERR_UNSUPPORTED, "scorer type has no density preselection");
+    if (nFrames > s->lastFrames)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "n_frames exceeds the frames of the last score call");
+    GMM_HIP_CHECK(hipSetDevice(s->device));
+    GMM_HIP_CHECK(hipDeviceSynchronize());
+    const uint32_t        nC     = s->clustering.nClusters;
+    const uint32_t        blocks = (nFrames + 63) / 64;
+    std::vector<uint32_t> words(static_cast<size_t>(blocks) * nC * 16);
+    if (!words.empty())
+        GMM_HIP_CHECK(hipMemcpy(words.data(), s->dSelT, words.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t t = 0; t < nFrames; ++t)
+        for (uint32_t c = 0; c < nC; ++c) {
+            const uint32_t w = words[(static_cast<size_t>(t / 64) * nC + c) * 16 + t % 16];
+            selection[static_cast<size_t>(t) * nC + c] = ((w >> (8 * ((t % 64) / 16))) & 0xffu) == 0 ? 1 : 0;
+        }
+    return GMM_OK;
+}
+
+int gmm_density_clustering_seeds(uint32_t nEntries, uint32_t nClusters, uint32_t* seeds) {
+    if (!seeds || nClusters == 0 || nClusters > nEntries)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "need 0 < n_clusters <= n_entries and an output array");
+    const std::vector<uint32_t> v = clusteringSeeds(nEntries, nClusters);
+    std::copy(v.begin(), v.end(), seeds);
     return GMM_OK;
 }
 

@@ -36,6 +36,11 @@ struct I8Args {
     uint32_t        idxBits;
     int             flavor;       // 0 SIMD-diagonal-maximum, 1 batch-int
     float           s2, batchScale, outScale;
+    // preselection-batch-int (gmm_kernels_presel.hip): per-(frame, cluster) mask, per-row cluster offsets
+    const uint32_t* selT;         // [nFramesPad/64][nClusters][16] u32, byte (frame%64)/16 = 0xff: deselected
+    const void*     tileClu;      // u16 [T+pad][16]: cluster * 64 (byte offset into a wave's mask table)
+    uint32_t        nClusters;
+    int             presel;
 };
 
 struct F32Args {
@@ -94,6 +99,12 @@ struct SplitArgs {
     uint32_t        tileBits;
     float           offsetK0;
     float           outScale;
+    // preselection-batch-float: as I8Args; a mixture without a selected density scores backoff
+    const uint32_t* selT;
+    const void*     tileClu;
+    uint32_t        nClusters;
+    int             presel;
+    float           backoff;
 };
 
 hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
@@ -110,6 +121,16 @@ hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps, 
 hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps, hipStream_t stream);  // diagonal-sum, 16-row tiles
 constexpr uint32_t kSplit32MaxKSteps = 10;  // 32-row split kernel instantiated for K/16 <= 10 (D <= 51)
 hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
+constexpr uint32_t kI8PreselNF           = 4;  // preselection-batch-int: 64 frames per wave (one mask word)
+constexpr uint32_t kI8PreselFramesPerBlock = kWavesPerBlock * kI8PreselNF * 16;
+
+// density preselection (gmm_kernels_presel.hip)
+hipError_t launchAssignDensities(bool quantized, const void* means, uint32_t nDensities, uint32_t Dp,
+                                 const void* clusterMeans, uint32_t nClusters, uint8_t* clusterOf, hipStream_t stream);
+hipError_t launchSelectClusters(bool quantized, const float* frames, uint32_t nFrames, uint32_t frameStride,
+                                uint32_t nFramesRead, uint32_t D, uint32_t Dp, const float* variance,
+                                const void* clusterMeans, uint32_t nClusters, uint32_t nSelected, uint32_t* selT,
+                                hipStream_t stream);
 hipError_t launchScoreF32(const F32Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 
 }  // namespace rasr_gmm

@@ -311,20 +311,33 @@ __global__ __launch_bounds__(256) void scoreI8(I8Args a) {
 // ---------------------------------------------------------------------------
 constexpr int kSegTiles = 8;
 
+// preselection-batch-int: the segment ring and the waves' mask tables share one dynamic LDS array
+extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
+
 // mixTileOff / scores / best are separate __restrict__ parameters so the mixture boundaries are read
 // with scalar loads (a vector load would need an s_waitcnt vmcnt(0) that drains the LDS-DMA queue).
-template <int NF, int KS>
+//
+// PRESEL (preselection-batch-int, NF = 4: one 64-frame mask word per wave): keys are biased by 2^31
+// (the packed row constant XOR 2^31) and compared unsigned, so OR-ing the sign-extended mask byte of a
+// (frame, density cluster) that the frame did not select makes the all-ones key, which never wins; the
+// segment carries each tile's 16 row offsets into the wave's mask table (gmm_kernels_presel.hip).
+template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles>
 __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
                                                    float* __restrict__ scores, uint32_t* __restrict__ bestOut) {
     static_assert(NF == 4 || NF == 8, "NF");
+    static_assert(!PRESEL || NF == 4, "preselection masks are 64-frame words");
+    constexpr int      kSegTiles = SEG;
     constexpr int      NPL       = NF / 4;
     constexpr uint32_t kTileA    = KS * 1024;                   // operand bytes per tile
     constexpr uint32_t kSegA     = kSegTiles * kTileA;
-    constexpr uint32_t kSegBytes = kSegA + kSegTiles * 64;      // + packed row constants
+    constexpr uint32_t kSegP     = kSegA + kSegTiles * 64;      // + packed row constants
+    constexpr uint32_t kSegBytes = kSegP + (PRESEL ? kSegTiles * 32 : 0);  // + row cluster offsets (u16)
     constexpr int      kPieces   = kSegTiles * KS / 4;          // 1 KiB pieces per wave per segment
+    constexpr int      kIssued   = kPieces + 1 + (PRESEL ? 1 : 0);  // vector memory ops per wave per segment
     static_assert(kSegTiles * KS % 4 == 0, "segment pieces must split evenly over 4 waves");
     // one __shared__ array only (a second one can make hipcc drain vmcnt before LDS reads)
-    __shared__ __attribute__((aligned(16))) int8_t lds[2 * kSegBytes];
+    __shared__ __attribute__((aligned(16))) int8_t ldsStatic[PRESEL ? 16 : 2 * kSegBytes];
+    int8_t* const lds = PRESEL ? i8DynLds : ldsStatic;
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -339,6 +352,8 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
     const uint32_t nSeg = (T1 - T0 + kSegTiles - 1) / kSegTiles;
     const int8_t*  gA   = static_cast<const int8_t*>(a.tileA);
     const int8_t*  gP   = static_cast<const int8_t*>(a.tileP);
+    const int8_t*  gClu = static_cast<const int8_t*>(a.tileClu);
+    (void)gClu;
 
     // issue segment s into buffer (s & 1); tile arrays are padded by kTilePad >= kSegTiles tiles
     const auto issueSeg = [&](uint32_t s) {
@@ -350,9 +365,14 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
             __builtin_amdgcn_global_load_lds(gA + static_cast<size_t>(t0) * kTileA + piece * 1024u + lane * 16,
                                              base + piece * 1024u, 16, 0, 0);
         }
-        if (lane < 8)  // 8 tiles x 64 B of row constants: 128 B per wave
-            __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * 128 + lane * 16,
-                                             base + kSegA + wave * 128, 16, 0, 0);
+        if (lane < kSegTiles)  // kSegTiles tiles x 64 B of row constants: 16 kSegTiles B per wave
+            __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * (kSegTiles * 16) + lane * 16,
+                                             base + kSegA + wave * (kSegTiles * 16), 16, 0, 0);
+        if constexpr (PRESEL) {  // kSegTiles tiles x 32 B of row cluster offsets: 8 kSegTiles B per wave
+            if (lane < kSegTiles / 2)
+                __builtin_amdgcn_global_load_lds(gClu + static_cast<size_t>(t0) * 32 + wave * (kSegTiles * 8) + lane * 16,
+                                                 base + kSegP + wave * (kSegTiles * 8), 16, 0, 0);
+        }
     };
     if (nSeg > 0)
         issueSeg(0);
@@ -373,9 +393,49 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
     for (int i = 0; i < NPL; ++i)
         ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
 
+    // preselection: this wave's 64-frame mask table [cluster][16] after the segment ring
+    uint32_t laneSel = 0;  // byte offset of (wave table, column t = lane & 15)
+    if constexpr (PRESEL) {
+        const uint32_t words = a.nClusters * 16u;
+        const i32x4*   src   = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
+        i32x4*         dst   = reinterpret_cast<i32x4*>(lds + 2 * kSegBytes + static_cast<uint32_t>(wave) * words * 4u);
+        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u)
+            dst[i] = src[i];
+        laneSel = 2 * kSegBytes + (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
+    }
+    // a tile's row constants (biased by 2^31 under PRESEL) and mask words of this lane's 4 rows
+    const auto tileRows = [&](const int8_t* base, uint32_t lt, i32x4& P, uint32_t(&T)[4]) {
+        P = *reinterpret_cast<const i32x4*>(base + kSegA + lt * 64 + g * 16);
+        if constexpr (PRESEL) {
+            const uint2 cw = *reinterpret_cast<const uint2*>(base + kSegP + lt * 32 + g * 8);
+            const int8_t* tb = lds + laneSel;
+            T[0] = *reinterpret_cast<const uint32_t*>(tb + (cw.x & 0xffffu));
+            T[1] = *reinterpret_cast<const uint32_t*>(tb + (cw.x >> 16));
+            T[2] = *reinterpret_cast<const uint32_t*>(tb + (cw.y & 0xffffu));
+            T[3] = *reinterpret_cast<const uint32_t*>(tb + (cw.y >> 16));
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                P[r] = static_cast<int>(static_cast<uint32_t>(P[r]) ^ 0x80000000u);
+        }
+    };
+
     const uint32_t sh   = static_cast<uint32_t>(ib + 1);
     const auto     pack = [&](int acc, int p) {
         return static_cast<int>((static_cast<uint32_t>(acc) << sh) + static_cast<uint32_t>(p));
+    };
+    // candidate key: the packed value; PRESEL: biased, OR the mask byte of column block cb
+    const auto cand = [&](int acc, int p, uint32_t T, int cb) -> int {
+        if constexpr (PRESEL)
+            return static_cast<int>(static_cast<uint32_t>(pack(acc, p)) |
+                                    static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(T >> (8 * cb)))));
+        else
+            return pack(acc, p);
+    };
+    const auto min2 = [](int x, int y) {
+        if constexpr (PRESEL)
+            return static_cast<int>(min(static_cast<uint32_t>(x), static_cast<uint32_t>(y)));
+        else
+            return min(x, y);
     };
     int best[NF][4];
     const auto resetBest = [&]() {
@@ -383,14 +443,28 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                best[cb][r] = INT_MAX;
+                best[cb][r] = PRESEL ? -1 : INT_MAX;  // PRESEL: 0xffffffff = biased INT_MAX
+    };
+    const auto emit = [&](uint32_t mm) {
+        if constexpr (PRESEL) {
+            int unb[NF][4];
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    unb[cb][r] = static_cast<int>(static_cast<uint32_t>(best[cb][r]) ^ 0x80000000u);
+            emitMixtureI8<NF>(a, scores, bestOut, unb, mm, frame0, lane, g, ib, ssOut);
+        }
+        else {
+            emitMixtureI8<NF>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
+        }
     };
     resetBest();
     uint32_t m    = m0;
     uint32_t tEnd = mixTileOff[m0 + 1];
     // mixtures without tiles at the start of the chunk
     while (m < m1 && tEnd == T0) {
-        emitMixtureI8<NF>(a, scores, bestOut, best, m, frame0, lane, g, ib, ssOut);
+        emit(m);
         ++m;
         tEnd = m < m1 ? mixTileOff[m + 1] : T1;
     }
@@ -398,7 +472,7 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
     for (uint32_t s = 0; s < nSeg; ++s) {
         // this segment's pieces (issued one segment ago) have landed; the next segment's stay in flight
         if (s + 1 < nSeg)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPieces + 1) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kIssued) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -417,9 +491,11 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
                     A0[ks] = *reinterpret_cast<const i32x4*>(base + lt * kTileA + ks * 1024 + lane * 16);
                     A1[ks] = *reinterpret_cast<const i32x4*>(base + (lt + 1) * kTileA + ks * 1024 + lane * 16);
                 }
-                const i32x4 P0 = *reinterpret_cast<const i32x4*>(base + kSegA + lt * 64 + g * 16);
-                const i32x4 P1 = *reinterpret_cast<const i32x4*>(base + kSegA + (lt + 1) * 64 + g * 16);
-                i32x4       accA[NF], accB[NF];
+                i32x4    P0, P1;
+                uint32_t T0w[4] = {}, T1w[4] = {};
+                tileRows(base, lt, P0, T0w);
+                tileRows(base, lt + 1, P1, T1w);
+                i32x4 accA[NF], accB[NF];
 #pragma unroll
                 for (int cb = 0; cb < NF; ++cb) {
                     accA[cb] = i32x4{0, 0, 0, 0};
@@ -434,7 +510,8 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
                 for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        best[cb][r] = min(best[cb][r], min(pack(accA[cb][r], P0[r]), pack(accB[cb][r], P1[r])));
+                        best[cb][r] = min2(best[cb][r], min2(cand(accA[cb][r], P0[r], T0w[r], cb),
+                                                             cand(accB[cb][r], P1[r], T1w[r], cb)));
 #if GMM_I8_INTERLEAVE
 #pragma unroll
                 for (int i = 0; i < 2 * NF * KS; ++i) {
@@ -449,8 +526,10 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks)
                     A0[ks] = *reinterpret_cast<const i32x4*>(base + lt * kTileA + ks * 1024 + lane * 16);
-                const i32x4 P0 = *reinterpret_cast<const i32x4*>(base + kSegA + lt * 64 + g * 16);
-                i32x4       accA[NF];
+                i32x4    P0;
+                uint32_t T0w[4] = {};
+                tileRows(base, lt, P0, T0w);
+                i32x4 accA[NF];
 #pragma unroll
                 for (int cb = 0; cb < NF; ++cb) {
                     accA[cb] = i32x4{0, 0, 0, 0};
@@ -462,12 +541,12 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
                 for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        best[cb][r] = min(best[cb][r], pack(accA[cb][r], P0[r]));
+                        best[cb][r] = min2(best[cb][r], cand(accA[cb][r], P0[r], T0w[r], cb));
                 t += 1;
             }
             // mixture(s) ending here (further ones without tiles end at the same point)
             while (t == tEnd && m < m1) {
-                emitMixtureI8<NF>(a, scores, bestOut, best, m, frame0, lane, g, ib, ssOut);
+                emit(m);
                 resetBest();
                 ++m;
                 tEnd = m < m1 ? mixTileOff[m + 1] : T1;
@@ -497,6 +576,21 @@ template <int NF, int KS, bool MULTI>
 static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
 #if GMM_I8_LDS
     if constexpr (!MULTI) {
+        if (a.presel) {  // preselection-batch-int: NF 4, 4-tile segments (ring + 4 mask tables < 80 KiB)
+            constexpr int      kSeg  = 4;
+            constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 32));
+            const uint32_t     lds   = kRing + 4u * a.nClusters * 64u;
+            static bool        attr  = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          static_cast<int>(kRing + 4u * 256u * 64u));
+                attr = true;
+            }
+            hipLaunchKernelGGL((dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>), dim3(grid), dim3(256), lds, s, a,
+                               a.mixTileOff, a.scores, a.best);
+            return;
+        }
         hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff, a.scores, a.best);
         return;
     }
@@ -508,6 +602,8 @@ hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStr
     const uint32_t grid = 8u * ((a.nChunks + 7u) / 8u) * a.nFrameTiles;
     if (grid == 0)
         return hipSuccess;
+    if (a.presel && (multiCov || !GMM_I8_LDS || a.nClusters == 0 || a.nClusters > 256 || !a.selT || !a.tileClu))
+        return hipErrorInvalidValue;
     if (kSteps == 1)
         multiCov ? launchI8T<kI8NF, 1, true>(a, grid, stream) : launchI8T<kI8NF, 1, false>(a, grid, stream);
     else if (kSteps == 2)

@@ -211,7 +211,13 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
 // loads (mixTileOff is a restrict kernel argument): a vector load there would come with an
 // s_waitcnt vmcnt(0) draining the prefetch.
 // ---------------------------------------------------------------------------
-template <int KS, bool BEST>
+// PRESEL (preselection-batch-float): every key is OR-ed with the sign-extended mask byte of its
+// (frame, density cluster), so a density whose cluster the frame did not select becomes the all-ones
+// key and never wins; the wave's mask table (gmm_kernels_presel.hip) sits in LDS, a tile carries the
+// 16 rows' table offsets, and a pair's 8 mask words are read in the step that issues its MFMAs.
+extern __shared__ __attribute__((aligned(16))) uint32_t splitSelLds[];
+
+template <int KS, bool BEST, bool PRESEL>
 __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
                                                                       const uint32_t* __restrict__ mixTileOff) {
     constexpr int  NF   = 4;
@@ -226,11 +232,35 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
     const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
 
+    // preselection: this wave's 64-frame mask table [cluster][16] into LDS (each wave reads only its own)
+    uint32_t laneSel = 0;  // byte address of (wave table, column t = lane & 15)
+    if constexpr (PRESEL) {
+        const uint32_t words = a.nClusters * 16u;
+        const u32x4*   src   = reinterpret_cast<const u32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
+        u32x4*         dst   = reinterpret_cast<u32x4*>(splitSelLds + static_cast<uint32_t>(wave) * words);
+        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u)
+            dst[i] = src[i];
+        laneSel = (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
+    }
+    const uint2* tclu = static_cast<const uint2*>(a.tileClu);
+
     const f16x8* th       = static_cast<const f16x8*>(a.tileH);
-    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS]) {
+    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS], uint2& Cw) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
             A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+        if constexpr (PRESEL)
+            Cw = tclu[static_cast<size_t>(tt) * 4 + g];  // rows 4g .. 4g+3: cluster * 64, u16 each
+    };
+    // the mask words of a tile's 4 rows in this lane (column frame0 + 16 cb + (lane & 15), byte cb)
+    const auto readSel = [&](const uint2& Cw, uint32_t(&T)[4]) {
+        if constexpr (PRESEL) {
+            const char* base = reinterpret_cast<const char*>(splitSelLds) + laneSel;
+            T[0]             = *reinterpret_cast<const uint32_t*>(base + (Cw.x & 0xffffu));
+            T[1]             = *reinterpret_cast<const uint32_t*>(base + (Cw.x >> 16));
+            T[2]             = *reinterpret_cast<const uint32_t*>(base + (Cw.y & 0xffffu));
+            T[3]             = *reinterpret_cast<const uint32_t*>(base + (Cw.y >> 16));
+        }
     };
 
     const f16x8* fh = static_cast<const f16x8*>(a.frameH);
@@ -253,18 +283,21 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
 
     // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
     f16x8 R0[KS], R1[KS], R2[KS], R3[KS];
-    loadTile(T0, R0);
-    loadTile(T0 + 1, R1);
-    loadTile(T0 + 2, R2);
-    loadTile(T0 + 3, R3);
+    uint2 C0{0, 0}, C1{0, 0}, C2{0, 0}, C3{0, 0};
+    loadTile(T0, R0, C0);
+    loadTile(T0 + 1, R1, C1);
+    loadTile(T0 + 2, R2, C2);
+    loadTile(T0 + 3, R3, C3);
 
     const uint32_t kmask = (1u << a.tileBits) - 1u;
     // the value mask lives in a VGPR so that (bits & mask) | tag is ONE v_and_or_b32 with the tag in an
     // SGPR (gfx950 VOP3 reads at most one SGPR)
     uint32_t vmask = ~kmask;
     asm volatile("" : "+v"(vmask));
-    // score of a mixture without a finite candidate: Core::Type<Score>::max, halved by diagonal-maximum
-    const float noneScore = __fmul_rn(a.outScale, a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f);
+    // score of a mixture without a finite candidate: Core::Type<Score>::max, halved by diagonal-maximum;
+    // preselection: the backoff score (BatchFeatureScorer.cc:282-288)
+    const float noneScore = __fmul_rn(a.outScale, PRESEL ? a.backoff
+                                                         : (a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f));
 
     uint32_t   best[NF][4];
     const auto resetBest = [&]() {
@@ -284,8 +317,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             for (int cb = 0; cb < NF; ++cb)
                 acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
     };
-    // epilogue of one pair of tiles (tile numbers tl, tl + 1 in the mixture)
-    const auto pairEpilogue = [&](const f32x4(&acc)[2][NF], uint32_t tl) {
+    // epilogue of one pair of tiles (tile numbers tl, tl + 1 in the mixture); TT: their mask words
+    const auto pairEpilogue = [&](const f32x4(&acc)[2][NF], uint32_t tl, const uint32_t(&TT)[2][4]) {
         // per-slot tags as opaque SGPRs: with a visible constant the compiler splits the tag OR off the
         // v_and_or_b32 into a v_and + v_or3 pair (non-volatile asm: no scheduling barrier)
         uint32_t tagA[4], tagB[4];
@@ -303,7 +336,14 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
                                                          : (__float_as_uint(acc[0][cb][r]) & vmask) | tagA[r];
                 const uint32_t kb = (GMM_SPLIT_DIAG & 2) ? __float_as_uint(acc[1][cb][r])
                                                          : (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
-                best[cb][r]       = umin3(best[cb][r], ka, kb);
+                if constexpr (PRESEL) {
+                    const uint32_t pa = static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[0][r] >> (8 * cb))));
+                    const uint32_t pb = static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[1][r] >> (8 * cb))));
+                    best[cb][r]       = umin3(best[cb][r], ka | pa, kb | pb);
+                }
+                else {
+                    best[cb][r] = umin3(best[cb][r], ka, kb);
+                }
             }
     };
 
@@ -326,17 +366,22 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     };
     // one pipeline step: the MFMAs of the pair in (A0, A1) into cur beside the epilogue of the pair in
     // prev, interleaved 1 MFMA : 2 VALU (the operand loads for two pairs ahead follow, then finish())
+    // (PRESEL: the mask words of the pair in (C0w, C1w) are read into TTcur; TTprev are prev's)
+    constexpr int kIl = PRESEL ? 28 : 24, kIlV = PRESEL ? 3 : 2;
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
-                          const f32x4(&prev)[2][NF], uint32_t tPrev) {
+                          const f32x4(&prev)[2][NF], uint32_t tPrev, const uint2& C0w, const uint2& C1w,
+                          uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) {
         chain(A0, cur[0]);
         chain(A1, cur[1]);
-        pairEpilogue(prev, tPrev - tBeg);
+        readSel(C0w, TTcur[0]);
+        readSel(C1w, TTcur[1]);
+        pairEpilogue(prev, tPrev - tBeg, TTprev);
 #pragma unroll
-        for (int i = 0; i < 24; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+        for (int i = 0; i < kIl; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, kIlV, 0);  // VALU
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 32 - kIl, 0);
     };
     // the emit of the mixture that ended at tile tNext, if any (a separate block: with the emit inside
     // the interleaved one, the duplicated step needs more than 256 VGPRs)
@@ -348,8 +393,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         }
     };
     // the last pair's epilogue (nothing left to overlap it with)
-    const auto drain = [&](const f32x4(&prev)[2][NF], uint32_t tPrev) {
-        pairEpilogue(prev, tPrev - tBeg);
+    const auto drain = [&](const f32x4(&prev)[2][NF], uint32_t tPrev, const uint32_t(&TTprev)[2][4]) {
+        pairEpilogue(prev, tPrev - tBeg, TTprev);
         finish(tPrev + 2);
     };
 
@@ -361,29 +406,32 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     }
     if (T0 < T1) {
         f32x4    accX[2][NF], accY[2][NF];
+        uint32_t TTX[2][4] = {}, TTY[2][4] = {};
         uint32_t t = T0;
         chain(R0, accX[0]);  // pair 0: nothing to finish beside it
         chain(R1, accX[1]);
-        loadTile(t + 4, R0);
-        loadTile(t + 5, R1);
+        readSel(C0, TTX[0]);
+        readSel(C1, TTX[1]);
+        loadTile(t + 4, R0, C0);
+        loadTile(t + 5, R1, C1);
         t += 2;
         for (; t + 4 <= T1; t += 4) {
-            step(R2, R3, accY, accX, t - 2);
-            loadTile(t + 4, R2);
-            loadTile(t + 5, R3);
+            step(R2, R3, accY, accX, t - 2, C2, C3, TTY, TTX);
+            loadTile(t + 4, R2, C2);
+            loadTile(t + 5, R3, C3);
             finish(t);
-            step(R0, R1, accX, accY, t);
-            loadTile(t + 6, R0);
-            loadTile(t + 7, R1);
+            step(R0, R1, accX, accY, t, C0, C1, TTX, TTY);
+            loadTile(t + 6, R0, C0);
+            loadTile(t + 7, R1, C1);
             finish(t + 2);
         }
         if (t < T1) {  // one more pair (in R2, R3)
-            step(R2, R3, accY, accX, t - 2);
+            step(R2, R3, accY, accX, t - 2, C2, C3, TTY, TTX);
             finish(t);
-            drain(accY, t);
+            drain(accY, t, TTY);
         }
         else {
-            drain(accX, t - 2);
+            drain(accX, t - 2, TTX);
         }
     }
 }
@@ -826,10 +874,21 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
 
 template <int KS>
 static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
-    if (a.best)
-        hipLaunchKernelGGL((dev::scoreSplit<KS, true>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+    if (a.presel) {  // preselection-batch-float: no best density; the waves' mask tables in dynamic LDS
+        const uint32_t lds = kSplitWaves * a.nClusters * 64u;
+        static bool    attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::scoreSplit<KS, false, true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSplitWaves * 256u * 64u));
+            attr = true;
+        }
+        hipLaunchKernelGGL((dev::scoreSplit<KS, false, true>), dim3(grid), dim3(64 * kSplitWaves), lds, s, a,
+                           a.mixTileOff);
+    }
+    else if (a.best)
+        hipLaunchKernelGGL((dev::scoreSplit<KS, true, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
     else
-        hipLaunchKernelGGL((dev::scoreSplit<KS, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit<KS, false, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
 }
 
 template <int KS>
@@ -844,6 +903,8 @@ hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps16
     const uint32_t grid = 8u * ((a.nChunks + 7u) / 8u) * a.nFrameTiles;
     if (grid == 0)
         return hipSuccess;
+    if (a.presel && (rows != 16 || a.nClusters == 0 || a.nClusters > 256 || !a.selT || !a.tileClu))
+        return hipErrorInvalidValue;  // the mask tables are laid out for 16-row tiles and <= 256 clusters
     if (rows == 32) {
         switch (kSteps16) {
             case 1: launchSplit32K<1>(a, grid, stream); break;

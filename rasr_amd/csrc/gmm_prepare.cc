@@ -500,8 +500,9 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
                 st        = std::move(pt);
                 fillEntry = std::move(pf);
             }
-            out.tiling      = std::move(st);
-            const uint32_t TP = out.tiling.nTiles;
+            out.tiling         = std::move(st);
+            out.splitFillEntry = fillEntry;
+            const uint32_t TP  = out.tiling.nTiles;
             for (uint32_t s = 0; s < kSplitLimbs; ++s)
                 out.limbExp[s] = b0 - 11 * static_cast<int32_t>(s);
             // per-dimension power of two that puts max|m''_d| in [2^7, 2^8): m'' and x'' then sit in

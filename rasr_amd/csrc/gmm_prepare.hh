@@ -91,6 +91,7 @@ struct PreparedFloat {
     Tiling             tiling;
     std::vector<float> tileA;         // [nTiles][kSteps][64 lanes]  (empty when split)
     std::vector<float> isvDevice;     // [C][kSteps*4] zero padded
+    std::vector<uint32_t> splitFillEntry; // split tiling: [tile] the entry its padding rows repeat
     // split-f16 kernel (single covariance, gmm_kernels_split.hip): every f32 operand is a sum of
     // two f16 pieces, hi + lo; a row is  sum_d [mh*xh + mh*xl + ml*xh]  +  sum_s limb_s * 2^(b_s)
     bool                  split    = false;

@@ -31,7 +31,8 @@ class Scorer:
     def __init__(self, mixture_set: MixtureSet, scorer_type="SIMD-diagonal-maximum", max_frames: int = 4096,
                  device: int = 0, mixture_weight_scale: float = 1.0, gaussian_scale: float = 1.0,
                  score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None, native_f32: bool = False,
-                 split_tile16: bool = False, split_tile32: bool = False):
+                 split_tile16: bool = False, split_tile32: bool = False, clusters: int = 256,
+                 select_clusters: int = 32, clustering_iterations: int = 5, backoff_score: float = 40000.0):
         self._lib = _capi.load_library()
         self.mixture_set = mixture_set
         self.type = _type_id(scorer_type)
@@ -46,6 +47,11 @@ class Scorer:
             cfg.flags |= _capi.GMM_FLAG_SPLIT_TILE16
         if split_tile32:  # split-f16 kernel: force 32-density tiles (mixtures <= 512 densities, D <= 51)
             cfg.flags |= _capi.GMM_FLAG_SPLIT_TILE32
+        # density preselection ("density-clustering" parameters, preselection-batch-* types)
+        cfg.clusters = int(clusters)
+        cfg.select_clusters = int(select_clusters)
+        cfg.clustering_iterations = int(clustering_iterations)
+        cfg.backoff_score = float(backoff_score)
         if mixture_range is not None:
             cfg.mixture_begin, cfg.mixture_end = int(mixture_range[0]), int(mixture_range[1])
         self.max_frames = int(max_frames)
@@ -78,6 +84,31 @@ class Scorer:
         _capi.check(self._lib.gmm_scorer_launch_info(self._h, 1, ctypes.byref(n), ctypes.byref(name)),
                     "gmm_scorer_launch_info")
         return name.value.decode()
+
+    def density_clustering(self):
+        """(cluster_of_entry [entries] u8, cluster_means [clusters][Dp] f32 or u8) of a preselection type."""
+        n = ctypes.c_uint32()
+        dp = ctypes.c_uint32()
+        _capi.check(self._lib.gmm_scorer_density_clustering(self._h, ctypes.byref(n), ctypes.byref(dp), None, None),
+                    "gmm_scorer_density_clustering")
+        entries = int(self.mixture_set.mixture_offsets[-1])
+        coe = np.zeros(entries, np.uint8)
+        dtype = np.uint8 if self.type == _capi.BATCH_PRESELECTION_INT else np.float32
+        means = np.zeros((n.value, dp.value), dtype)
+        _capi.check(self._lib.gmm_scorer_density_clustering(self._h, None, None, coe.ctypes.data_as(ctypes.c_void_p),
+                                                            means.ctypes.data_as(ctypes.c_void_p)),
+                    "gmm_scorer_density_clustering")
+        return coe, means
+
+    def cluster_selection(self, n_frames: int) -> np.ndarray:
+        """The [n_frames][clusters] 0/1 selection of the last score call (synchronizes)."""
+        n = ctypes.c_uint32()
+        _capi.check(self._lib.gmm_scorer_density_clustering(self._h, ctypes.byref(n), None, None, None),
+                    "gmm_scorer_density_clustering")
+        sel = np.zeros((int(n_frames), n.value), np.uint8)
+        _capi.check(self._lib.gmm_scorer_cluster_selection(self._h, int(n_frames), sel.ctypes.data_as(ctypes.c_void_p)),
+                    "gmm_scorer_cluster_selection")
+        return sel
 
     def n_mixtures(self) -> int:
         return int(self._lib.gmm_scorer_n_mixtures(self._h))
