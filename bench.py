@@ -48,8 +48,12 @@ MODES = {
     "simd": ("SIMD-diagonal-maximum", "s8xs8->i32 (u8-quantized, bit-exact)"),
     "sum": ("diagonal-sum", "f32"),  # log-sum-exp variant (GaussDiagonalSumFeatureScorer), --mode sum
     "nn": ("nn-batch-feature-scorer", "bf16 x bf16 -> f32 (MFMA), f32 bias/activation"),  # config 5, --mode nn
+    # density preselection (256 clusters, 32 selected per frame): cluster selection + masked scoring
+    "presel-float": ("preselection-batch-float", "f32"),
+    "presel-int": ("preselection-batch-int", "s8xs8->i32 (u8-quantized, bit-exact)"),
 }
-DEFAULT_FRAMES = {"fp32": 32768, "simd": 32768, "sum": 32768, "nn": 32768}  # frames per GPU per step (batch)
+DEFAULT_FRAMES = {"fp32": 32768, "simd": 32768, "sum": 32768, "nn": 32768, "presel-float": 32768,
+                  "presel-int": 32768}  # frames per GPU per step (batch)
 # BASELINE config 5 network (hybrid DNN): 11 x 39 spliced MFCC input, 6 sigmoid layers of 2048, 5000 classes
 NN_DIMS = [429] + [2048] * 6 + [5000]
 
@@ -138,7 +142,8 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
     m_local = sc.n_mixtures()
     frames = torch.from_numpy(ra.synthetic_frames(frames_per_gpu, args.dim, seed=seed)).to(dev)
     scores = torch.empty((m_local, frames_per_gpu), dtype=torch.float32, device=dev)
-    best = None if args.no_best else torch.empty((m_local, frames_per_gpu), dtype=torch.int32, device=dev)
+    best = None if (args.no_best or mode.startswith("presel")) else torch.empty((m_local, frames_per_gpu), dtype=torch.int32,
+                                                                                   device=dev)
     stream = torch.cuda.current_stream(dev)
 
     def step():

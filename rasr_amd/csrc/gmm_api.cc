@@ -474,6 +474,10 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         s->multiCov        = s->C > 1;
         s->nTiles          = p.tiling.nTiles;
         s->mixTileOff      = p.tiling.mixTileOffset;
+        // preselection-batch-int compares keys biased by 2^31 as unsigned (gmm_kernels_i8.hip, PRESEL)
+        if (presel)
+            for (int32_t& v : p.tileP)
+                v = static_cast<int32_t>(static_cast<uint32_t>(v) ^ 0x80000000u);
         // one zero padding tile so the kernels may prefetch tile t+1 unconditionally
         // kTilePad zero tiles at the end: the kernels prefetch two tiles ahead without bound checks
         if ((rc = upload(reinterpret_cast<int8_t**>(&s->dTileA), p.tileA, kTilePad * kLanes * 16 * p.kSteps)) ||

@@ -403,7 +403,7 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
             dst[i] = src[i];
         laneSel = 2 * kSegBytes + (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
     }
-    // a tile's row constants (biased by 2^31 under PRESEL) and mask words of this lane's 4 rows
+    // a tile's row constants (the host biases them by 2^31 for PRESEL) and mask words of this lane's 4 rows
     const auto tileRows = [&](const int8_t* base, uint32_t lt, i32x4& P, uint32_t(&T)[4]) {
         P = *reinterpret_cast<const i32x4*>(base + kSegA + lt * 64 + g * 16);
         if constexpr (PRESEL) {
@@ -413,9 +413,6 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
             T[1] = *reinterpret_cast<const uint32_t*>(tb + (cw.x >> 16));
             T[2] = *reinterpret_cast<const uint32_t*>(tb + (cw.y & 0xffffu));
             T[3] = *reinterpret_cast<const uint32_t*>(tb + (cw.y >> 16));
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                P[r] = static_cast<int>(static_cast<uint32_t>(P[r]) ^ 0x80000000u);
         }
     };
 

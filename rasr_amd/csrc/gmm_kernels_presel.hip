@@ -10,8 +10,9 @@
 //                    distances summed in the reference order, strict < keeps the first nearest);
 //   selectClusters   selectClusters per frame: the distance to every cluster, the rank of each
 //                    distance by counting, and -- only for a frame with a tie across the selection
-//                    boundary -- a replay of the reference's std::sort (gmm_refsort.hh), so the
-//                    selection equals the reference's also on ties.
+//                    boundary -- a replay of the reference's std::sort along the partition path that
+//                    holds the boundary (gmm_refsort.hh), so the selection equals the reference's also
+//                    on ties.
 //
 // Mask layout (read by the scorers' lanes straight from LDS): for every block of 64 frames, every
 // cluster c and t = frame % 16 one u32 whose byte cb = (frame % 64) / 16 is 0x00 (c selected) or 0xff
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(256) void selectClusters(const float* __restrict__ 
         for (uint32_t j = 0; j < nClusters; ++j)
             idx[f][j] = static_cast<uint8_t>(j);
         RefSortRange<Dist, uint8_t> s{dist[f], idx[f]};
-        s.sort(static_cast<int>(nClusters));
+        s.selectFirst(static_cast<int>(nClusters), static_cast<int>(nSelected));  // the set sort leaves in [0, k)
         for (uint32_t j = 0; j < nClusters; ++j)
             sel[f][j] = 0;
         for (uint32_t i = 0; i < nSelected; ++i)

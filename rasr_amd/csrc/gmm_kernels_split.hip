@@ -337,9 +337,13 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
                 const uint32_t kb = (GMM_SPLIT_DIAG & 2) ? __float_as_uint(acc[1][cb][r])
                                                          : (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
                 if constexpr (PRESEL) {
-                    const uint32_t pa = static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[0][r] >> (8 * cb))));
-                    const uint32_t pb = static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[1][r] >> (8 * cb))));
-                    best[cb][r]       = umin3(best[cb][r], ka | pa, kb | pb);
+                    // tag | sign-extended mask byte (one v_or_b32_sdwa), made opaque so that the key stays
+                    // one v_and_or_b32 (else the three ORs fold into v_or3 beside a separate v_and + v_bfe)
+                    uint32_t ca = tagA[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[0][r] >> (8 * cb))));
+                    uint32_t cc = tagB[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[1][r] >> (8 * cb))));
+                    asm("" : "+v"(ca), "+v"(cc));
+                    best[cb][r] = umin3(best[cb][r], (__float_as_uint(acc[0][cb][r]) & vmask) | ca,
+                                        (__float_as_uint(acc[1][cb][r]) & vmask) | cc);
                 }
                 else {
                     best[cb][r] = umin3(best[cb][r], ka, kb);

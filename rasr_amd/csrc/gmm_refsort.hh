@@ -164,6 +164,38 @@ struct RefSortRange {
         }
     }
 
+    // The set std::sort(key, key + n) leaves in positions [0, k), without the rest of the sort: after a
+    // partition every element of [first, cut) is <= every element of [cut, last), and the final
+    // insertion sort moves an element only past strictly greater ones, so no element ever leaves the
+    // introsort range it ends up in.  Ranges entirely left or right of k are therefore decided, and only
+    // the one range containing the boundary is followed (a single partition path, like quickselect):
+    // down to <= 16 elements, whose final order is the stable (insertion) order of their positions,
+    // or to the depth-limit heapsort, replayed in full.  Positions [0, k) then hold the selection.
+    GMM_HD void selectFirst(int n, int k) {
+        if (k <= 0 || k >= n)
+            return;
+        constexpr int kThreshold = 16;
+        int           lg         = 0;
+        while ((2 << lg) <= n)
+            ++lg;
+        int first = 0, last = n, depth = 2 * lg;
+        while (last - first > kThreshold) {
+            if (depth == 0) {
+                heapSort(first, last);
+                return;
+            }
+            --depth;
+            const int cut = unguardedPartitionPivot(first, last);
+            if (cut <= k)      // [first, cut) all selected; the boundary is in the recursion on [cut, last)
+                first = cut;
+            else               // the loop continues on [first, cut)
+                last = cut;
+            if (first == k)    // the cut fell on the boundary
+                return;
+        }
+        insertionSort(first, last);
+    }
+
     // std::sort(key, key + n) carrying idx along
     GMM_HD void sort(int n) {
         if (n <= 0)

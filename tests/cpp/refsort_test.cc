@@ -97,6 +97,43 @@ int main() {
                     }
                 ++cases;
             }
+    // selectFirst(n, k): the set std::sort leaves in [0, k)
+    for (int n : {2, 3, 16, 17, 40, 100, 255, 256})
+        for (int range : {0, 1, 3, 10, 100, 1 << 30})
+            for (int rep = 0; rep < 30; ++rep) {
+                std::vector<std::pair<int, unsigned>> ref(n);
+                std::vector<int>                      key0(n);
+                std::uniform_int_distribution<int>    d(0, range);
+                for (int i = 0; i < n; ++i) {
+                    key0[i] = d(rng);
+                    ref[i]  = std::make_pair(key0[i], static_cast<unsigned>(i));
+                }
+                std::sort(ref.begin(), ref.end(), [](const std::pair<int, unsigned>& x, const std::pair<int, unsigned>& y) {
+                    return x.first < y.first;
+                });
+                for (int k : {1, 2, 5, 16, 17, 32, n / 2, n - 1}) {
+                    if (k <= 0 || k >= n)
+                        continue;
+                    std::vector<int>           key(key0);
+                    std::vector<unsigned char> idx(n);
+                    for (int i = 0; i < n; ++i)
+                        idx[i] = static_cast<unsigned char>(i);
+                    rasr_gmm::RefSortRange<int, unsigned char> s{key.data(), idx.data()};
+                    s.selectFirst(n, k);
+                    std::vector<unsigned> a, b;
+                    for (int i = 0; i < k; ++i) {
+                        a.push_back(ref[i].second);
+                        b.push_back(idx[i]);
+                    }
+                    std::sort(a.begin(), a.end());
+                    std::sort(b.begin(), b.end());
+                    if (a != b) {
+                        std::printf("selectFirst mismatch n=%d k=%d range=%d\n", n, k, range);
+                        ++fails;
+                    }
+                    ++cases;
+                }
+            }
     std::printf("refsort: %d cases, %d failures\n", cases, fails);
     return fails ? 1 : 0;
 }
