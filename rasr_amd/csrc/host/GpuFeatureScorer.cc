@@ -91,6 +91,8 @@ static bool typeOf(const std::string& name, gmm_scorer_type* t, bool* assigning,
             {"batch-diagonal-maximum-int", GMM_BATCH_DIAGONAL_MAXIMUM_INT, false, true},
             {"batch-diagonal-maximum-fast", GMM_BATCH_DIAGONAL_MAXIMUM_FAST, false, true},
             {"batch-diagonal-maximum-float", GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT, false, true},
+            {"preselection-batch-float", GMM_BATCH_PRESELECTION_FLOAT, false, true},
+            {"preselection-batch-int", GMM_BATCH_PRESELECTION_INT, false, true},
     };
     for (const auto& e : table)
         if (name == e.name) {
@@ -121,6 +123,10 @@ bool FeatureScorer::init(const MixtureSet& ms, const Configuration& c, uint32_t 
     cfg.gaussian_scale       = c.gaussianScale;
     cfg.score_scale          = c.scale;
     cfg.max_frames           = maxFrames;
+    cfg.clusters              = c.clusters;
+    cfg.select_clusters       = c.selectClusters;
+    cfg.clustering_iterations = c.clusteringIterations;
+    cfg.backoff_score         = c.backoffScore;
     const gmm_mixture_set d  = ms.descriptor();
     if (gmm_scorer_create(&d, t, &cfg, c.device, &handle_) != GMM_OK) {
         if (error)

@@ -82,6 +82,11 @@ struct Configuration {
     float       gaussianScale      = 1.0f;  // "gaussian-scale" (GDMFS.cc:42-44)
     float       scale              = 1.0f;  // FeatureScorerScaling scale (ScaledFeatureScorer.hh:62-64)
     int         device             = 0;
+    // "density-clustering" of the preselection scorers (DensityClustering.cc:19-32)
+    uint32_t clusters             = 256;
+    uint32_t selectClusters       = 32;
+    uint32_t clusteringIterations = 5;
+    float    backoffScore         = 40000.0f;
 };
 
 // ---------------------------------------------------------------------------

@@ -108,3 +108,18 @@ def test_simd_protocol_model_from_pms_file(gpu, tmp_path):
     ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
     assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
     assert np.array_equal(b.T, ref_b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["preselection-batch-int", "preselection-batch-float"])
+def test_preselection_protocol(gpu, tmp_path, kind):
+    # the ring-buffer protocol with the default density-clustering parameters (256 clusters, 32 selected)
+    ms = ra.synthetic_mixture_set(40, 12, 39, seed=47, weights="random")
+    frames = ra.synthetic_frames(37, 39, seed=48)
+    s, _, _ = _run(tmp_path, ms, frames, kind, 4, 2)
+    ref = oracle.OraclePresel(ms, "int" if kind.endswith("int") else "float").score(frames)
+    if kind.endswith("int"):
+        assert np.array_equal(s.T.view(np.uint32), ref.view(np.uint32))
+    else:
+        err = np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))
+        assert err.max() <= 1e-4
