@@ -22,7 +22,7 @@ HDRS      = include/rasr_gmm.h $(SRC)/gmm_presel.hh $(SRC)/gmm_prepare.hh $(SRC)
 LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
             $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
-            $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o
+            $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o $(BUILD)/gmm_kernels_shard.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 REFSORT   = $(BUILD)/tests/refsort_test
@@ -43,6 +43,11 @@ $(BUILD)/gmm_kernels_split.o: $(SRC)/gmm_kernels_split.hip $(HDRS)
 
 # density preselection: clustering assignment + per-frame cluster selection (std::sort replay)
 $(BUILD)/gmm_kernels_presel.o: $(SRC)/gmm_kernels_presel.hip $(SRC)/gmm_refsort.hh $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# density-sharded exchange keys (BASELINE config 4)
+$(BUILD)/gmm_kernels_shard.o: $(SRC)/gmm_kernels_shard.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -10,7 +10,7 @@ bit-exact SIMD-diagonal-maximum scorer (int8 MFMA) is timed too and reported
 under "modes".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fp32|simd] [--frames F]
-                  [--parallel frames|mixtures]
+                  [--parallel frames|mixtures|densities]
 
 N > 1 is launched by torch.distributed.run, one process per GPU:
   --parallel frames   (default; configs 2-3): every rank scores its own F frames
@@ -19,7 +19,11 @@ N > 1 is launched by torch.distributed.run, one process per GPU:
   --parallel mixtures (config 4): every rank holds 1/N of the mixtures (density
                       balanced) and scores the same F frames; the [M][F] score
                       table is assembled with one all-gather over RCCL per step,
-                      "scaling": "strong".
+                      "scaling": "strong";
+  --parallel densities (config 4 as written): every rank holds 1/N of the densities
+                      (mixtures on shard boundaries split between ranks) and scores
+                      the same F frames; whole mixtures all-gathered, split ones
+                      reduced per frame with an RCCL all-reduce(MIN), "strong".
 A barrier + synchronize brackets the timed region; the max over ranks is reported.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP events
@@ -65,7 +69,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--mode", choices=sorted(MODES), default="fp32")
     p.add_argument("--frames", type=int, default=0, help="frames per GPU per step (default: mode-specific)")
-    p.add_argument("--parallel", choices=["frames", "mixtures"], default="frames")
+    p.add_argument("--parallel", choices=["frames", "mixtures", "densities"], default="frames")
     p.add_argument("--mixtures", type=int, default=5000)
     p.add_argument("--densities", type=int, default=160)
     p.add_argument("--dim", type=int, default=39)
@@ -130,9 +134,12 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
     from rasr_amd import parallel
     kind, dtype = MODES[mode]
     dev = torch.device("cuda", local)
-    sharded = args.parallel == "mixtures" and ws > 1
+    sharded = args.parallel in ("mixtures", "densities") and ws > 1
     if sharded:
-        scorer = parallel.MixtureShardedScorer(ms, kind, frames_per_gpu, rank, ws, device=local)
+        if args.parallel == "densities":
+            scorer = parallel.DensityShardedScorer(ms, kind, frames_per_gpu, rank, ws, device=local)
+        else:
+            scorer = parallel.MixtureShardedScorer(ms, kind, frames_per_gpu, rank, ws, device=local)
         sc = scorer.scorer
         seed = 1000  # every rank scores the same frames
     else:
@@ -166,8 +173,13 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
     dt_max = max_over_ranks(dt, ws)
     kms_avg = max_over_ranks(kms / max(nl, 1), ws)
     total_frames = (1 if sharded else ws) * frames_per_gpu * args.steps
-    d_local = int(ms.mixture_offsets[min(ms.n_mixtures, scorer.shards[rank][1])]
-                  - ms.mixture_offsets[scorer.shards[rank][0]]) if sharded else int(ms.n_entries)
+    if sharded and args.parallel == "densities":
+        d_local = scorer.shards[rank]["entries"][1] - scorer.shards[rank]["entries"][0]
+    elif sharded:
+        d_local = int(ms.mixture_offsets[min(ms.n_mixtures, scorer.shards[rank][1])]
+                      - ms.mixture_offsets[scorer.shards[rank][0]])
+    else:
+        d_local = int(ms.n_entries)
     algo = 2.0 * args.dim * d_local * frames_per_gpu  # one multiply-add per (frame, density, component)
     kernel = sc.main_kernel()
     split = kernel in ("scoreSplit", "scoreSplit32", "scoreSplitSum")
@@ -320,7 +332,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": res["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "strong" if (args.parallel == "mixtures" and ws > 1) else "weak",
+            "scaling": "strong" if (args.parallel in ("mixtures", "densities") and ws > 1) else "weak",
             "vs_baseline": None,
             "dtype": res["dtype"],
             "data": "synthetic (SURVEY 8(d): means N(0,1), var 0.5+|N(0,1)|, frames N(0,1))",
@@ -332,9 +344,10 @@ def main():
                 "densities_per_mixture": args.densities,
                 "dimension": args.dim,
                 "frames_per_gpu_per_step": frames_per_gpu,
-                "best_density": not args.no_best,
+                "best_density": not args.no_best and not args.mode.startswith("presel"),
                 "parallelism": (f"mixture-sharded x{ws} + RCCL all-gather" if args.parallel == "mixtures" and ws > 1
-                                else f"frame-sharded replicas x{ws}"),
+                                else f"density-sharded x{ws} + RCCL all-reduce(MIN) of split mixtures + all-gather"
+                                if args.parallel == "densities" and ws > 1 else f"frame-sharded replicas x{ws}"),
             },
             "roofline": res["roofline"],
             "cpu_baseline": cpu,

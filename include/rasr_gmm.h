@@ -172,6 +172,19 @@ int gmm_scorer_density_clustering(const gmm_scorer* scorer, uint32_t* n_clusters
 int gmm_scorer_cluster_selection(gmm_scorer* scorer, uint32_t n_frames, uint8_t* selection);
 int gmm_density_clustering_seeds(uint32_t n_entries, uint32_t n_clusters, uint32_t* seed_entries);
 
+/* Density-sharded layout (BASELINE config 4: a mixture's densities split over GPUs, per-frame reduce over
+ * RCCL).  The reference is single-process (no counterpart); these define the exchange format.
+ * gmm_shard_pack_keys: [rows][n_frames] int64 keys = (order-preserving score bits << 32) | (best density
+ *   + best_offset[row]), whose signed minimum is the reference's winner (lower score, then lower density
+ *   index); best / best_offset may be NULL (density 0 / offset 0).  An all-reduce(MIN) over the keys of
+ *   the GPUs holding parts of a mixture is the per-frame reduce.
+ * gmm_shard_unpack_keys: keys -> scores (and best densities if best != NULL).
+ * DEVICE pointers, row stride `stride` for scores/best, keys dense; asynchronous on `stream`. */
+int gmm_shard_pack_keys(const float* scores, const uint32_t* best, const uint32_t* best_offset, uint32_t rows,
+                        uint32_t n_frames, uint32_t stride, int64_t* keys, void* stream);
+int gmm_shard_unpack_keys(const int64_t* keys, uint32_t rows, uint32_t n_frames, float* scores, uint32_t* best,
+                          uint32_t stride, void* stream);
+
 const char* gmm_last_error(void);
 const char* gmm_version(void);
 

@@ -108,6 +108,12 @@ PROTOTYPES = [
      [ctypes.c_void_p, _u32p, _u32p, ctypes.c_void_p, ctypes.c_void_p]),
     ("gmm_scorer_cluster_selection", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     ("gmm_density_clustering_seeds", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, _u32p]),
+    ("gmm_shard_pack_keys", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_void_p, ctypes.c_void_p]),
+    ("gmm_shard_unpack_keys", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+      ctypes.c_void_p]),
     ("gmm_last_error", ctypes.c_char_p, []),
     # include/rasr_gmm_io.h
     ("gmm_mixture_set_read", ctypes.c_int,

@@ -779,6 +779,26 @@ int gmm_density_clustering_seeds(uint32_t nEntries, uint32_t nClusters, uint32_t
     return GMM_OK;
 }
 
+int gmm_shard_pack_keys(const float* scores, const uint32_t* best, const uint32_t* bestOffset, uint32_t rows,
+                        uint32_t nFrames, uint32_t stride, int64_t* keys, void* stream) {
+    if (rows == 0 || nFrames == 0)
+        return GMM_OK;
+    if (!scores || !keys || stride < nFrames)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "invalid scores/keys/stride");
+    GMM_HIP_CHECK(launchPackShardKeys(scores, best, bestOffset, rows, nFrames, stride, keys, static_cast<hipStream_t>(stream)));
+    return GMM_OK;
+}
+
+int gmm_shard_unpack_keys(const int64_t* keys, uint32_t rows, uint32_t nFrames, float* scores, uint32_t* best,
+                          uint32_t stride, void* stream) {
+    if (rows == 0 || nFrames == 0)
+        return GMM_OK;
+    if (!scores || !keys || stride < nFrames)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "invalid scores/keys/stride");
+    GMM_HIP_CHECK(launchUnpackShardKeys(keys, rows, nFrames, scores, best, stride, static_cast<hipStream_t>(stream)));
+    return GMM_OK;
+}
+
 const char* gmm_last_error(void) {
     return gLastError.c_str();
 }

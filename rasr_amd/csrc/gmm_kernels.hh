@@ -124,6 +124,12 @@ hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStr
 constexpr uint32_t kI8PreselNF           = 4;  // preselection-batch-int: 64 frames per wave (one mask word)
 constexpr uint32_t kI8PreselFramesPerBlock = kWavesPerBlock * kI8PreselNF * 16;
 
+// density-sharded exchange (gmm_kernels_shard.hip): (score, density) <-> order-preserving int64 keys
+hipError_t launchPackShardKeys(const float* scores, const uint32_t* best, const uint32_t* bestOffset, uint32_t rows,
+                               uint32_t nFrames, uint32_t stride, int64_t* keys, hipStream_t stream);
+hipError_t launchUnpackShardKeys(const int64_t* keys, uint32_t rows, uint32_t nFrames, float* scores, uint32_t* best,
+                                 uint32_t stride, hipStream_t stream);
+
 // density preselection (gmm_kernels_presel.hip)
 hipError_t launchAssignDensities(bool quantized, const void* means, uint32_t nDensities, uint32_t Dp,
                                  const void* clusterMeans, uint32_t nClusters, uint8_t* clusterOf, hipStream_t stream);
