@@ -7,9 +7,12 @@
 
 namespace rasr_nn {
 
-constexpr uint32_t kNnTileM = 128;  // output units per workgroup tile
-constexpr uint32_t kNnTileN = 128;  // frames per workgroup tile
-constexpr uint32_t kNnTileK = 64;   // K per pipeline stage
+#ifndef NN_GEMM_TILE
+#define NN_GEMM_TILE 256  // 256: nnGemm256 (8 waves, 128 KiB LDS); 128: nnGemm (4 waves), kept for A/B
+#endif
+constexpr uint32_t kNnTileM = NN_GEMM_TILE;  // output units per workgroup tile
+constexpr uint32_t kNnTileN = NN_GEMM_TILE;  // frames per workgroup tile
+constexpr uint32_t kNnTileK = 64;            // K per pipeline stage
 
 // One layer: Out = act(A . B^T + bias) with A = W^T [Mpad][Kpad] (bf16 bits), B = layer input
 // [Npad][Kpad] (bf16 bits, frame-major).  Hidden layers store Y [Npad][Mpad] bf16 (the next

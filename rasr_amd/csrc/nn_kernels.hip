@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256) void nnPrepareInput(const float* __restrict__ 
     X[static_cast<size_t>(t) * Kpad + k] = toBf16(frames[static_cast<size_t>(t) * frameStride + k]);
 }
 
-__global__ __launch_bounds__(256, 2) void nnGemm(NnGemmArgs a) {
+__global__ __launch_bounds__(256) void nnGemm(NnGemmArgs a) {
+    constexpr uint32_t kNnTileM = 128, kNnTileN = 128, kNnTileK = 64;  // this kernel's tile (NN_GEMM_TILE 128)
     __shared__ __attribute__((aligned(16))) uint16_t lds[2][2][kNnTileM * kNnTileK];  // [stage][A|B], one array
 
     const int      lane = threadIdx.x & 63;
@@ -140,6 +141,184 @@ __global__ __launch_bounds__(256, 2) void nnGemm(NnGemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// nnGemm256: 256 x 256 output tile per 512-thread workgroup, 8 waves as 2 (units) x 4 (frames), each
+// wave 128 x 64 (8 x 4 accumulators of v_mfma_f32_16x16x32_bf16).  K advances in 64-wide tiles, two
+// LDS buffers of 64 KiB (A 256 rows | B 256 rows, 128-B rows) filled by global_load_lds_dwordx4 in
+// half-tiles of 128 rows (16 KiB: two 1-KiB wave-instructions per wave).  Per K-tile u (buffer u & 1):
+//   H0: stage A of tile u+1 (other buffer); s_waitcnt vmcnt(8) retires tile u (8 = the B of u+1 and
+//       A of u+1 issued after it); barrier; read the wave's A rows 0..63 and all its B rows; 32 MFMAs;
+//       barrier (B of buffer u & 1 free);
+//   H1: stage B of tile u+2 (this buffer); read A rows 64..127; 32 MFMAs; barrier (A free).
+// So B is prefetched ~3 half-steps and A ~2 ahead, one counted vmcnt per K-tile, never 0 in the loop
+// (0 only when no later tile exists).  LDS rows: the 16-B piece c of row r sits at c ^ ((r >> 1) & 7):
+// the 16 lanes of a ds_read_b128 group (16 consecutive rows, one piece) then hit 16 different 16-B
+// bank slots (two 128-B rows share a 256-B bank row), conflict-free.
+// ---------------------------------------------------------------------------
+extern __shared__ __attribute__((aligned(16))) uint16_t nnLds[];  // [2 buffers][A | B][256 * 64]
+
+#ifndef NN_GEMM_VARIANT
+#define NN_GEMM_VARIANT 0  // 0: three barriers per K-tile (H0 | H1); 1: reads front-loaded, two barriers
+#endif
+#ifndef NN_GEMM_SETPRIO
+#define NN_GEMM_SETPRIO 0  // s_setprio(1) around the MFMA clusters
+#endif
+#if NN_GEMM_SETPRIO
+#define NN_SETPRIO(x) __builtin_amdgcn_s_setprio(x)
+#else
+#define NN_SETPRIO(x) ((void)0)
+#endif
+
+__device__ __forceinline__ uint32_t nnSwz(uint32_t r) {
+    return (r >> 1) & 7u;
+}
+
+__global__ __launch_bounds__(512) void nnGemm256(NnGemmArgs a) {
+    constexpr uint32_t T = 256, BK = 64, kOp = T * BK;  // elements per operand image
+    const int          lane = threadIdx.x & 63;
+    const int          wave = threadIdx.x >> 6;
+    const uint32_t     nMT = a.Mpad / T, nNT = a.Npad / T, nwg = nMT * nNT;
+    const uint32_t     b = blockIdx.x, xcd = b & 7u, q = nwg / 8u, r = nwg % 8u;
+    const uint32_t     id = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (b >> 3);
+    const uint32_t     m0 = (id % nMT) * T, n0 = (id / nMT) * T;
+    const uint32_t     wr = static_cast<uint32_t>(wave) >> 2, wc = static_cast<uint32_t>(wave) & 3u;
+    const uint32_t     nK = a.Kpad / BK;
+
+    // half h (rows 128 h .. 128 h + 127) of operand op (0 = A, 1 = B) of K-tile u into buffer buf
+    const auto stage = [&](int op, uint32_t h, uint32_t u, uint32_t buf) {
+        const uint16_t* src  = op == 0 ? a.A : a.B;
+        const uint32_t  base = op == 0 ? m0 : n0;
+#pragma unroll
+        for (uint32_t i = 0; i < 2; ++i) {
+            const uint32_t p   = static_cast<uint32_t>(wave) * 128u + i * 64u + static_cast<uint32_t>(lane);
+            const uint32_t row = h * 128u + p / 8u;
+            const uint32_t c   = (p % 8u) ^ nnSwz(row);
+            __builtin_amdgcn_global_load_lds(src + static_cast<size_t>(base + row) * a.Kpad + u * BK + 8u * c,
+                                             nnLds + (buf * 2u + static_cast<uint32_t>(op)) * kOp + h * (kOp / 2) +
+                                                     (static_cast<uint32_t>(wave) * 128u + i * 64u) * 8u,
+                                             16, 0, 0);
+        }
+    };
+    const auto stageA = [&](uint32_t u, uint32_t buf) {
+        stage(0, 0, u, buf);
+        stage(0, 1, u, buf);
+    };
+    const auto stageB = [&](uint32_t u, uint32_t buf) {
+        stage(1, 0, u, buf);
+        stage(1, 1, u, buf);
+    };
+    const auto frag = [&](uint32_t buf, int op, uint32_t row, uint32_t ks) {
+        const uint32_t c = ks * 4u + (static_cast<uint32_t>(lane) >> 4);
+        return *reinterpret_cast<const bf16x8*>(nnLds + (buf * 2u + static_cast<uint32_t>(op)) * kOp + row * BK +
+                                                (c ^ nnSwz(row)) * 8u);
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    const uint32_t rl = static_cast<uint32_t>(lane) & 15u;
+    stageB(0, 0);
+    stageA(0, 0);
+    if (nK > 1)
+        stageB(1, 1);
+    for (uint32_t u = 0; u < nK; ++u) {
+        const uint32_t buf = u & 1u;
+        // H0
+        if (u + 1 < nK) {
+            stageA(u + 1, buf ^ 1u);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        }
+        else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of tile u are in LDS
+        bf16x8 fa[4][2], fb[4][2], fa2[4][2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                fb[j][ks] = frag(buf, 1, wc * 64u + 16u * j + rl, ks);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa[i][ks] = frag(buf, 0, wr * 128u + 16u * i + rl, ks);
+        }
+#if NN_GEMM_VARIANT == 1
+        // all of the tile's reads up front (A rows 64..127 too), 64 MFMAs, one closing barrier
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa2[i][ks] = frag(buf, 0, wr * 128u + 64u + 16u * i + rl, ks);
+#endif
+        NN_SETPRIO(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[i][j], 0, 0, 0);
+#if NN_GEMM_VARIANT == 0
+        NN_SETPRIO(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // B of this buffer read by every wave
+        // H1
+        if (u + 2 < nK)
+            stageB(u + 2, buf);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa2[i][ks] = frag(buf, 0, wr * 128u + 64u + 16u * i + rl, ks);
+        NN_SETPRIO(1);
+#endif
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa2[i][ks], fb[j][ks], acc[4 + i][j], 0, 0, 0);
+        NN_SETPRIO(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // A (and B) of this buffer read by every wave
+#if NN_GEMM_VARIANT == 1
+        if (u + 2 < nK)
+            stageB(u + 2, buf);
+#endif
+    }
+
+    // epilogue: rows m = m0 + 128 wr + 16 i + 4 (lane >> 4) + rr, frame n = n0 + 64 wc + 16 j + (lane & 15)
+    const uint32_t g = static_cast<uint32_t>(lane) >> 4, col = rl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t mb = m0 + wr * 128u + 16u * i + 4u * g;
+        const f32x4    bs = *reinterpret_cast<const f32x4*>(a.bias + mb);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t n = n0 + wc * 64u + 16u * j + col;
+            if (a.top) {
+                if (n < a.nFrames)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        if (mb + rr < a.M)
+                            a.scores[static_cast<size_t>(mb + rr) * a.scoreStride + n] = -(acc[i][j][rr] + bs[rr]);
+            }
+            else {
+                u16x4 v;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    v[rr] = toBf16(activate(acc[i][j][rr] + bs[rr], a.act, a.gamma));
+                *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
+            }
+        }
+    }
+}
+
 }  // namespace dev
 
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
@@ -158,7 +337,21 @@ hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream) {
     const uint32_t nwg = (a.Mpad / kNnTileM) * (a.Npad / kNnTileN);
     if (nwg == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(dev::nnGemm, dim3(nwg), dim3(256), 0, stream, a);
+    if constexpr (kNnTileM == 256) {
+        constexpr uint32_t kLds = 2u * 2u * 256u * 64u * 2u;  // 128 KiB
+        static bool        attr = false;
+        if (!attr) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::nnGemm256),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLds));
+            if (e != hipSuccess)
+                return e;
+            attr = true;
+        }
+        hipLaunchKernelGGL(dev::nnGemm256, dim3(nwg), dim3(512), kLds, stream, a);
+    }
+    else {
+        hipLaunchKernelGGL(dev::nnGemm, dim3(nwg), dim3(256), 0, stream, a);
+    }
     return hipGetLastError();
 }
 
