@@ -3,7 +3,8 @@
 // the epilogue.
 //
 // GEMM: C[M x N] = A[M x K] . B[N x K]^T, A = W^T (output units x inputs), B = activations (frames x
-// inputs), both K-contiguous, so both MFMA operands are 16-byte row pieces.  A 256-thread workgroup
+// inputs), both K-contiguous, so both MFMA operands are 16-byte row pieces.  Production kernel:
+// nnGemm256 below (NN_GEMM_TILE 256).  nnGemm (NN_GEMM_TILE 128, kept for A/B): a 256-thread workgroup
 // computes a 128 x 128 tile as 2 x 2 waves of 64 x 64 (4 x 4 v_mfma_f32_16x16x32_bf16 accumulators);
 // K advances in 64-wide stages staged global -> LDS by global_load_lds_dwordx4 (each wave issues 4 x
 // 1 KiB for A and for B), double-buffered: the next stage's DMA is in flight while the current one is
