@@ -84,14 +84,23 @@ def parse():
 
 
 def dist_setup():
+    """One process per GPU over RCCL ("nccl").  Rehearsal only (not used by the driver): with
+    RASR_BENCH_SAME_DEVICE=1 every rank uses GPU 0 and RASR_BENCH_BACKEND=gloo replaces RCCL, so the
+    N > 1 flow can be exercised on a one-GPU box."""
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RASR_BENCH_SAME_DEVICE") == "1":
+        local = 0
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("RASR_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
@@ -266,7 +275,7 @@ def run_nn(args, ws, rank, local, frames_per_gpu):
         "frames_per_gpu": frames_per_gpu,
         "roofline": {
             "bound": "mfma", "achieved": algo / sec / 1e12, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": algo / sec / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None, "kernel": "nnGemm",
+            "frac": algo / sec / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None, "kernel": "nnGemm256",
             "kernel_ms": kms_avg, "algorithmic_flop_per_launch": algo, "issued_mfma_flop_per_launch": issued,
             "issued_mfma_tflops": issued / sec / 1e12,
         },
