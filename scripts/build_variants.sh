@@ -5,7 +5,9 @@
 # -> rasr_amd/lib/variants/librasr_gmm_<name>.so (same host objects, different kernel objects)
 set -e
 cd "$(dirname "$0")/.."
-make -s build/gmm_api.o build/gmm_prepare.o build/GpuFeatureScorer.o build/MixtureSetFile.o build/nn_kernels.o build/nn_api.o
+make -s all
+# every object except the kernel TUs and the API TU rebuilt per variant below
+OTHER=$(ls build/*.o | grep -v -E "gmm_kernels_(i8|f32|split)\.o|gmm_api\.o")
 mkdir -p rasr_amd/lib/variants build/variants
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off"
 while [ $# -ge 3 ]; do
@@ -16,6 +18,6 @@ while [ $# -ge 3 ]; do
   defs=$(echo "$i8 $f32" | tr ' ' '\n' | grep '^-D' | tr '\n' ' ')
   /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -ffp-contract=off $defs -c rasr_amd/csrc/gmm_api.cc -o build/variants/api_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o rasr_amd/lib/variants/librasr_gmm_$name.so \
-      build/variants/i8_$name.o build/variants/f32_$name.o build/variants/split_$name.o build/variants/api_$name.o build/gmm_prepare.o build/GpuFeatureScorer.o build/MixtureSetFile.o build/nn_kernels.o build/nn_api.o -lz
+      build/variants/i8_$name.o build/variants/f32_$name.o build/variants/split_$name.o build/variants/api_$name.o $OTHER -lz
   echo built $name
 done
