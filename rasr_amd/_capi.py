@@ -138,6 +138,15 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         raise RuntimeError(
             f"rasr_amd native library not found at {p}: the MI355X scorer has no fallback; "
             "build it with `make` (or __graft_entry__.build())")
+    # Two HIP runtimes end up in a Python process: the image's ROCm (librasr_gmm.so's libamdhip64.so.7)
+    # and the one bundled with torch.  When librasr_gmm.so is loaded before torch, torch's HIP calls partly
+    # bind to the ROCm copy and, once torch has initialised the device, hipGetDeviceCount in the ROCm copy
+    # fails ("no HIP device available"; scripts/debug/probe_order.py).  Loading torch first keeps each
+    # library on its own runtime.  (C++ callers such as RASR have one runtime and are unaffected.)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(p)
     for name, res, args in PROTOTYPES:
         fn = getattr(lib, name)

@@ -41,7 +41,11 @@ def cpu_vendor():
 
 
 def main():
+    # default tests/golden; `--out DIR` writes a set for another CPU's rsqrtss (e.g. made on the GPU box
+    # into gpurun_out/ and committed as tests/golden/cpu_<vendor>/), so the GPU tests there are not skipped
     out = os.path.join(ROOT, "tests", "golden")
+    if "--out" in sys.argv:
+        out = os.path.abspath(sys.argv[sys.argv.index("--out") + 1])
     os.makedirs(out, exist_ok=True)
     for name, kw in CASES.items():
         ms = ra.synthetic_mixture_set(**kw)

@@ -13,7 +13,10 @@ import pytest
 import oracle
 import rasr_amd as ra
 
-GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+# tests/golden/*.npz: made in the build container; tests/golden/cpu_*/*.npz: the same cases made by the
+# oracle on another host CPU (its rsqrtss), e.g. the GPU box's (scripts/make_golden.py --out)
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")) +
+                glob.glob(os.path.join(os.path.dirname(__file__), "golden", "cpu_*", "*.npz")))
 
 
 def _load(path):
