@@ -256,6 +256,32 @@ __global__ __launch_bounds__(512) void nnGemm256(NnGemmArgs a) {
                 fa2[i][ks] = frag(buf, 0, wr * 128u + 64u + 16u * i + rl, ks);
 #endif
         NN_SETPRIO(1);
+#if NN_GEMM_VARIANT == 2
+        // A rows 64..127 read in the middle of the first half's MFMAs (latency hidden behind 16 MFMAs)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa2[i][ks] = frag(buf, 0, wr * 128u + 64u + 16u * i + rl, ks);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+        NN_SETPRIO(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // B of this buffer read by every wave
+        if (u + 2 < nK)
+            stageB(u + 2, buf);
+        NN_SETPRIO(1);
+#else
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -263,18 +289,30 @@ __global__ __launch_bounds__(512) void nnGemm256(NnGemmArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[i][j], 0, 0, 0);
-#if NN_GEMM_VARIANT == 0
+#endif
+#if NN_GEMM_VARIANT == 0 || NN_GEMM_VARIANT == 3
         NN_SETPRIO(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // B of this buffer read by every wave
-        // H1
-        if (u + 2 < nK)
-            stageB(u + 2, buf);
+#if NN_GEMM_VARIANT == 3
+        // A rows 64..127 read behind the first half's MFMAs, before the barrier
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 fa2[i][ks] = frag(buf, 0, wr * 128u + 64u + 16u * i + rl, ks);
+#endif
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // B of this buffer read by every wave
+        // H1
+        if (u + 2 < nK)
+            stageB(u + 2, buf);
+#if NN_GEMM_VARIANT == 0
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa2[i][ks] = frag(buf, 0, wr * 128u + 64u + 16u * i + rl, ks);
+#endif
         NN_SETPRIO(1);
 #endif
 #pragma unroll
