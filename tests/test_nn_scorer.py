@@ -79,3 +79,18 @@ def test_nn_scorer_device_strides_and_errors(gpu):
     with pytest.raises(ra.GmmError):
         nn.NnScorer([(np.ones((4, 5), np.float32), None, "relu", 1.0),
                      (np.ones((6, 2), np.float32), None, "identity", 1.0)])  # 5 != 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,frames", [([100, 70], 300),      # K 100 -> 2 K-tiles of 64
+                                          ([150, 64, 33], 257),  # 3 K-tiles, then 4 (padded 256)
+                                          ([64, 600, 10], 513),  # exactly 1 K-tile, then 12
+                                          ([1, 5], 3)])          # a 1-wide input
+def test_nn_scorer_k_tile_counts(gpu, dims, frames):
+    # the GEMM's pipeline has separate paths for the last one and two K-tiles (no later stage to issue,
+    # s_waitcnt vmcnt(0) instead of the counted wait): every short K-tile count is exercised
+    layers = nn.synthetic_network(dims, "tanh", seed=sum(dims))
+    x = ra.synthetic_frames(frames, dims[0], seed=frames + 1)
+    sc = nn.NnScorer(layers, max_frames=frames)
+    s = sc.score_host(x)
+    assert _err(s, nn_oracle.forward_bf16(layers, x).astype(np.float64)) <= 2e-3
