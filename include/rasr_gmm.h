@@ -124,9 +124,18 @@ int      gmm_scorer_type_of(const gmm_scorer* scorer);
 int gmm_score_device(gmm_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
                      float* scores, uint32_t* best_density, uint32_t score_stride, void* stream);
 
-/* Same with HOST buffers (copies in, scores, copies out, synchronizes). */
+/* Same with HOST buffers (copies in, scores, copies out, synchronizes).  Large batches are scored in
+ * frame chunks with the copy-out of one chunk overlapped with the scoring of the next; a score/best
+ * buffer from gmm_host_alloc (or otherwise page-locked) is written by DMA directly, a pageable one
+ * through a pinned staging ring and RASR_GMM_HOST_THREADS copy threads (default 8). */
 int gmm_score_host(gmm_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
                    float* scores, uint32_t* best_density, uint32_t score_stride);
+
+/* Page-locked host memory for gmm_score_host's outputs (the buffer a batched caller keeps, e.g.
+ * BatchFeatureScorerBase::scores_, BatchFeatureScorer.hh:177-186), so that callers need no HIP
+ * headers.  gmm_host_free(NULL) is a no-op. */
+int gmm_host_alloc(size_t bytes, void** ptr);
+int gmm_host_free(void* ptr);
 
 /* SimdGaussDiagonalMaximumFeatureScorer accessors used by AcousticLookAhead
  * (src/Search/AdvancedTreeSearch/AcousticLookAhead.cc:156,447):

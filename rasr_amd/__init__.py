@@ -8,11 +8,11 @@ from ._capi import (BATCH_DIAGONAL_MAXIMUM_FAST, BATCH_DIAGONAL_MAXIMUM_FLOAT, B
                     DIAGONAL_MAXIMUM, LIB_PATH, SCORER_TYPES, SIMD_DIAGONAL_MAXIMUM, GmmError, load_library)
 from .mixture_set import (MixtureSet, parse_mixture_set, ragged_counts, read_mixture_set, synthetic_frames,
                           synthetic_mixture_set, write_mixture_set)
-from .scorer import Scorer, default_config, prepare_quantized_host
+from .scorer import Scorer, default_config, pinned_empty, prepare_quantized_host
 
 __all__ = [
     "BATCH_DIAGONAL_MAXIMUM_FAST", "BATCH_DIAGONAL_MAXIMUM_FLOAT", "BATCH_DIAGONAL_MAXIMUM_INT", "DIAGONAL_MAXIMUM",
     "SIMD_DIAGONAL_MAXIMUM", "SCORER_TYPES", "LIB_PATH", "GmmError", "load_library", "MixtureSet", "ragged_counts",
-    "synthetic_frames", "synthetic_mixture_set", "Scorer", "default_config", "prepare_quantized_host",
+    "synthetic_frames", "synthetic_mixture_set", "Scorer", "default_config", "pinned_empty", "prepare_quantized_host",
     "read_mixture_set", "parse_mixture_set", "write_mixture_set",
 ]

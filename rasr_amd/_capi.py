@@ -94,6 +94,8 @@ PROTOTYPES = [
     ("gmm_score_host", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
       ctypes.c_uint32]),
+    ("gmm_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("gmm_host_free", ctypes.c_int, [ctypes.c_void_p]),
     ("gmm_scorer_quantization", ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p]),
     ("gmm_scorer_multiply_and_quantize", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("gmm_prepare_quantized_host", ctypes.c_int,

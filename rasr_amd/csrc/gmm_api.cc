@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/rasr_gmm.h"
+#include "gmm_hostio.hh"
 #include "gmm_kernels.hh"
 #include "gmm_prepare.hh"
 #include "gmm_presel.hh"
@@ -114,6 +115,15 @@ struct gmm_scorer {
     float*    dHostFrames = nullptr;
     float*    dHostScores = nullptr;
     uint32_t* dHostBest   = nullptr;
+    // gmm_score_host pipeline (large calls): scoring and copy-out streams, one event per frame chunk,
+    // a double-buffered pinned staging ring for pageable destinations and its copy threads
+    hipStream_t                   hostCompute = nullptr, hostCopy = nullptr;
+    hipEvent_t                    hostStart   = nullptr;
+    std::vector<hipEvent_t>       chunkDone;
+    hipEvent_t                    stageDone[2] = {nullptr, nullptr};
+    void*                         hStage       = nullptr;  // 2 x hStageBytes, hipHostMalloc
+    size_t                        hStageBytes  = 0;
+    std::unique_ptr<HostCopyPool> copyPool;
     std::map<uint32_t, ChunkTable> chunks;  // keyed by frame tiles per call
     // kernel timing (gmm_scorer_set_timing)
     bool                                        timing = false;
@@ -134,6 +144,16 @@ struct gmm_scorer {
             (void)hipEventDestroy(ev.first);
             (void)hipEventDestroy(ev.second);
         }
+        for (hipEvent_t ev : chunkDone)
+            (void)hipEventDestroy(ev);
+        for (hipEvent_t ev : {hostStart, stageDone[0], stageDone[1]})
+            if (ev)
+                (void)hipEventDestroy(ev);
+        for (hipStream_t st : {hostCompute, hostCopy})
+            if (st)
+                (void)hipStreamDestroy(st);
+        if (hStage)
+            (void)hipHostFree(hStage);
     }
 };
 
@@ -409,6 +429,137 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
     return GMM_OK;
 }
 
+// gmm_score_host for large calls (score table >= kHostPipelineBytes).  The batch is scored in frame
+// chunks on hostCompute; the copy-out of chunk k on hostCopy overlaps the scoring of chunk k+1.  A
+// pinned destination is written by the DMA engines directly.  A pageable one goes through a pinned
+// double-buffered staging ring: the D2H of piece j+1 is in flight while the copy threads move piece j
+// into the caller's rows (the runtime's own pageable path is one thread, ~10 GB/s).
+constexpr size_t   kHostPipelineBytes = size_t(8) << 20;
+constexpr uint32_t kHostChunkFrames   = 8192;
+constexpr uint32_t kHostMaxChunks     = 8;
+constexpr size_t   kHostStageBytes    = size_t(16) << 20;
+
+int ensureHostPipeline(gmm_scorer* s, uint32_t nChunks) {
+    if (!s->hostCompute) {
+        GMM_HIP_CHECK(hipStreamCreateWithFlags(&s->hostCompute, hipStreamNonBlocking));
+        GMM_HIP_CHECK(hipStreamCreateWithFlags(&s->hostCopy, hipStreamNonBlocking));
+        GMM_HIP_CHECK(hipEventCreateWithFlags(&s->hostStart, hipEventDisableTiming));
+        for (hipEvent_t& ev : s->stageDone)
+            GMM_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    while (s->chunkDone.size() < nChunks) {
+        hipEvent_t ev = nullptr;
+        GMM_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        s->chunkDone.push_back(ev);
+    }
+    return GMM_OK;
+}
+
+int ensureHostStage(gmm_scorer* s, size_t rowBytes) {
+    const size_t want = std::max(kHostStageBytes, rowBytes);
+    if (s->hStageBytes >= want)
+        return GMM_OK;
+    if (s->hStage)
+        GMM_HIP_CHECK(hipHostFree(s->hStage));
+    s->hStage      = nullptr;
+    s->hStageBytes = 0;
+    GMM_HIP_CHECK(hipHostMalloc(&s->hStage, 2 * want, hipHostMallocDefault));
+    s->hStageBytes = want;
+    if (!s->copyPool)
+        s->copyPool.reset(new HostCopyPool(hostCopyThreads()));
+    return GMM_OK;
+}
+
+int scoreHostPipelined(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+                       uint32_t* best, uint32_t scoreStride) {
+    const uint32_t fpb = framesPerBlock(s);
+    // one chunk for preselection: gmm_scorer_cluster_selection reports the last call's whole batch
+    uint32_t nChunks = s->presel ? 1u : std::clamp<uint32_t>(nFrames / kHostChunkFrames, 1u, kHostMaxChunks);
+    const uint32_t per = ((nFrames + nChunks - 1) / nChunks + fpb - 1) / fpb * fpb;
+    nChunks            = (nFrames + per - 1) / per;
+    int rc             = ensureHostPipeline(s, nChunks);
+    if (rc != GMM_OK)
+        return rc;
+    const size_t D = s->D;
+    // after the legacy stream's earlier work (gmm_score_device callers on stream 0 share the staging)
+    GMM_HIP_CHECK(hipEventRecord(s->hostStart, nullptr));
+    GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCompute, s->hostStart, 0));
+    GMM_HIP_CHECK(hipMemcpy2DAsync(s->dHostFrames, D * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
+                                   D * sizeof(float), nFrames, hipMemcpyHostToDevice, s->hostCompute));
+    for (uint32_t k = 0; k < nChunks; ++k) {
+        const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
+        rc = scoreImpl(s, s->dHostFrames + t0 * D, n, s->D, s->dHostScores + t0, best ? s->dHostBest + t0 : nullptr, nFrames,
+                       s->hostCompute);
+        if (rc != GMM_OK)
+            return rc;
+        GMM_HIP_CHECK(hipEventRecord(s->chunkDone[k], s->hostCompute));
+    }
+
+    struct Table {
+        char*       dst;
+        const char* src;
+    };
+    std::vector<Table> direct, staged;
+    for (Table t : {Table{reinterpret_cast<char*>(scores), reinterpret_cast<const char*>(s->dHostScores)},
+                    Table{reinterpret_cast<char*>(best), reinterpret_cast<const char*>(s->dHostBest)}})
+        if (t.dst)
+            (isPinnedHost(t.dst) ? direct : staged).push_back(t);
+    const size_t dPitch = static_cast<size_t>(scoreStride) * 4, sPitch = static_cast<size_t>(nFrames) * 4;
+    for (uint32_t k = 0; k < nChunks; ++k) {
+        const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
+        GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCopy, s->chunkDone[k], 0));
+        for (const Table& t : direct)
+            GMM_HIP_CHECK(hipMemcpy2DAsync(t.dst + static_cast<size_t>(t0) * 4, dPitch, t.src + static_cast<size_t>(t0) * 4,
+                                           sPitch, static_cast<size_t>(n) * 4, s->nMix, hipMemcpyDeviceToHost,
+                                           s->hostCopy));
+    }
+    if (!staged.empty()) {
+        if ((rc = ensureHostStage(s, static_cast<size_t>(per) * 4)) != GMM_OK)
+            return rc;
+        struct Piece {
+            uint32_t k, t0, n, r0, r1;
+            Table    t;
+        };
+        std::vector<Piece> pieces;
+        for (uint32_t k = 0; k < nChunks; ++k) {
+            const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
+            const uint32_t rows = static_cast<uint32_t>(std::max<size_t>(1, s->hStageBytes / (static_cast<size_t>(n) * 4)));
+            for (const Table& t : staged)
+                for (uint32_t r0 = 0; r0 < s->nMix; r0 += rows)
+                    pieces.push_back(Piece{k, t0, n, r0, std::min(s->nMix, r0 + rows), t});
+        }
+        char* stage[2] = {static_cast<char*>(s->hStage), static_cast<char*>(s->hStage) + s->hStageBytes};
+        auto  issue    = [&](size_t j) -> int {
+            const Piece& p = pieces[j];
+            if (j == 0 || pieces[j - 1].k != p.k)
+                GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCopy, s->chunkDone[p.k], 0));
+            GMM_HIP_CHECK(hipMemcpy2DAsync(stage[j & 1], static_cast<size_t>(p.n) * 4,
+                                           p.t.src + static_cast<size_t>(p.r0) * sPitch + static_cast<size_t>(p.t0) * 4, sPitch,
+                                           static_cast<size_t>(p.n) * 4, p.r1 - p.r0, hipMemcpyDeviceToHost, s->hostCopy));
+            GMM_HIP_CHECK(hipEventRecord(s->stageDone[j & 1], s->hostCopy));
+            return GMM_OK;
+        };
+        if ((rc = issue(0)) != GMM_OK)
+            return rc;
+        for (size_t j = 0; j < pieces.size(); ++j) {
+            // stage[(j+1)&1] was drained by the host copy of piece j-1 (synchronous, below)
+            if (j + 1 < pieces.size() && (rc = issue(j + 1)) != GMM_OK)
+                return rc;
+            GMM_HIP_CHECK(hipEventSynchronize(s->stageDone[j & 1]));
+            const Piece& p   = pieces[j];
+            const char*  src = stage[j & 1];
+            const size_t w   = static_cast<size_t>(p.n) * 4;
+            s->copyPool->parallelFor(p.r1 - p.r0, [&](size_t b, size_t e) {
+                for (size_t r = b; r < e; ++r)
+                    std::memcpy(p.t.dst + (p.r0 + r) * dPitch + static_cast<size_t>(p.t0) * 4, src + r * w, w);
+            });
+        }
+    }
+    GMM_HIP_CHECK(hipStreamSynchronize(s->hostCopy));
+    GMM_HIP_CHECK(hipStreamSynchronize(s->hostCompute));
+    return GMM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -617,6 +768,8 @@ int gmm_score_host(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostScores), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(float)));
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostBest), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(uint32_t)));
     }
+    if (static_cast<size_t>(nFrames) * std::max<uint32_t>(s->nMix, 1) * sizeof(float) >= kHostPipelineBytes)
+        return scoreHostPipelined(s, frames, nFrames, frameStride, scores, best, scoreStride);
     GMM_HIP_CHECK(hipMemcpy2D(s->dHostFrames, s->D * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
                               s->D * sizeof(float), nFrames, hipMemcpyHostToDevice));
     int rc = scoreImpl(s, s->dHostFrames, nFrames, s->D, s->dHostScores, best ? s->dHostBest : nullptr, nFrames, nullptr);
@@ -630,6 +783,22 @@ int gmm_score_host(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_
         GMM_HIP_CHECK(hipMemcpy2D(best, static_cast<size_t>(scoreStride) * sizeof(uint32_t), s->dHostBest,
                                   static_cast<size_t>(nFrames) * sizeof(uint32_t),
                                   static_cast<size_t>(nFrames) * sizeof(uint32_t), s->nMix, hipMemcpyDeviceToHost));
+    return GMM_OK;
+}
+
+int gmm_host_alloc(size_t bytes, void** ptr) {
+    if (!ptr)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null ptr");
+    *ptr = nullptr;
+    if (bytes == 0)
+        return GMM_OK;
+    GMM_HIP_CHECK(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
+    return GMM_OK;
+}
+
+int gmm_host_free(void* ptr) {
+    if (ptr)
+        GMM_HIP_CHECK(hipHostFree(ptr));
     return GMM_OK;
 }
 

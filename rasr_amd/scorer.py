@@ -130,15 +130,22 @@ class Scorer:
                                         int(scores.stride(0)), ctypes.c_void_p(s) if s else None)
         _capi.check(rc, "gmm_score_device")
 
-    def score_host(self, frames: np.ndarray, want_best: bool = True):
+    def score_host(self, frames: np.ndarray, want_best: bool = True, out: np.ndarray | None = None,
+                   best_out: np.ndarray | None = None):
+        """gmm_score_host.  out / best_out: caller-kept [n_mixtures][>= n_frames] tables (row stride =
+        their second dimension), e.g. from pinned_empty() so the table is written by DMA directly."""
         frames = np.ascontiguousarray(frames, dtype=np.float32)
         f = frames.shape[0]
         m = self.n_mixtures()
-        scores = np.empty((m, f), dtype=np.float32)
-        best = np.empty((m, f), dtype=np.uint32) if want_best else None
+        scores = np.empty((m, f), dtype=np.float32) if out is None else out
+        best = (np.empty((m, f), dtype=np.uint32) if best_out is None else best_out) if want_best else None
+        stride = scores.shape[1] if scores.ndim == 2 else f
+        for name, a, dt in (("out", scores, np.float32), ("best_out", best, np.uint32)):
+            if a is not None and (a.dtype != dt or a.shape != (m, stride) or not a.flags.c_contiguous or stride < f):
+                raise ValueError(f"{name} must be a C-contiguous {np.dtype(dt).name} [{m}][>= {f}] array")
         rc = self._lib.gmm_score_host(self._h, frames.ctypes.data_as(ctypes.c_void_p), f, frames.shape[1],
                                       scores.ctypes.data_as(ctypes.c_void_p),
-                                      best.ctypes.data_as(ctypes.c_void_p) if best is not None else None, f)
+                                      best.ctypes.data_as(ctypes.c_void_p) if best is not None else None, stride)
         _capi.check(rc, "gmm_score_host")
         return scores, best
 
@@ -166,6 +173,20 @@ class Scorer:
                                                                out.ctypes.data_as(ctypes.c_void_p)),
                     "gmm_scorer_multiply_and_quantize")
         return out
+
+
+def pinned_empty(shape, dtype=np.float32) -> np.ndarray:
+    """Uninitialised numpy array in page-locked host memory (gmm_host_alloc; freed with the array)."""
+    import weakref
+
+    lib = _capi.load_library()
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    ptr = ctypes.c_void_p()
+    _capi.check(lib.gmm_host_alloc(max(n, 1), ctypes.byref(ptr)), "gmm_host_alloc")
+    holder = (ctypes.c_char * max(n, 1)).from_address(ptr.value)
+    weakref.finalize(holder, lib.gmm_host_free, ptr.value)
+    return np.frombuffer(holder, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
 
 
 def prepare_quantized_host(ms: MixtureSet, scorer_type="SIMD-diagonal-maximum") -> dict:
