@@ -275,7 +275,7 @@ def run_nn(args, ws, rank, local, frames_per_gpu):
         "frames_per_gpu": frames_per_gpu,
         "roofline": {
             "bound": "mfma", "achieved": algo / sec / 1e12, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": algo / sec / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None, "kernel": "nnGemm256",
+            "frac": algo / sec / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None, "kernel": "nnGemm8p",
             "kernel_ms": kms_avg, "algorithmic_flop_per_launch": algo, "issued_mfma_flop_per_launch": issued,
             "issued_mfma_tflops": issued / sec / 1e12,
         },

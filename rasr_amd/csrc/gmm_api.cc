@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -186,7 +187,12 @@ int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
 #ifndef GMM_TARGET_BLOCKS
 #define GMM_TARGET_BLOCKS 8192
 #endif
-    const uint32_t kTargetBlocks = GMM_TARGET_BLOCKS;
+    // RASR_GMM_TARGET_BLOCKS: tuning override (scripts/sweep_chunks.sh)
+    static const uint32_t kTargetBlocks = [] {
+        const char* e = std::getenv("RASR_GMM_TARGET_BLOCKS");
+        const long  v = e ? std::strtol(e, nullptr, 10) : 0;
+        return v > 0 ? static_cast<uint32_t>(v) : uint32_t(GMM_TARGET_BLOCKS);
+    }();
     uint32_t       target        = std::max<uint32_t>(1, (kTargetBlocks + nFrameTiles - 1) / nFrameTiles);
     target                       = std::min<uint32_t>(target, std::max<uint32_t>(1, s->nMix));
     const uint32_t T             = s->nTiles;

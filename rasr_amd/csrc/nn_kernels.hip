@@ -4,7 +4,7 @@
 //
 // GEMM: C[M x N] = A[M x K] . B[N x K]^T, A = W^T (output units x inputs), B = activations (frames x
 // inputs), both K-contiguous, so both MFMA operands are 16-byte row pieces.  Production kernel:
-// nnGemm256 below (NN_GEMM_TILE 256).  nnGemm (NN_GEMM_TILE 128, kept for A/B): a 256-thread workgroup
+// nnGemm8p below (NN_GEMM_TILE 256, NN_GEMM_VARIANT 8); nnGemm256 (the two-half schedule) is kept for A/B.  nnGemm (NN_GEMM_TILE 128, kept for A/B): a 256-thread workgroup
 // computes a 128 x 128 tile as 2 x 2 waves of 64 x 64 (4 x 4 v_mfma_f32_16x16x32_bf16 accumulators);
 // K advances in 64-wide stages staged global -> LDS by global_load_lds_dwordx4 (each wave issues 4 x
 // 1 KiB for A and for B), double-buffered: the next stage's DMA is in flight while the current one is
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void nnGemm(NnGemmArgs a) {
 extern __shared__ __attribute__((aligned(16))) uint16_t nnLds[];  // [2 buffers][A | B][256 * 64]
 
 #ifndef NN_GEMM_VARIANT
-#define NN_GEMM_VARIANT 0  // 0: three barriers per K-tile (H0 | H1); 1: reads front-loaded, two barriers
+#define NN_GEMM_VARIANT 8  // 8: nnGemm8p (production); 0: nnGemm256 three barriers per K-tile (H0 | H1); 1: reads front-loaded, two barriers
 #endif
 #ifndef NN_GEMM_SETPRIO
 #define NN_GEMM_SETPRIO 0  // s_setprio(1) around the MFMA clusters
@@ -358,6 +358,198 @@ __global__ __launch_bounds__(512) void nnGemm256(NnGemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// nnGemm8p: the same 256 x 256 tile, 8 waves, 128 KiB LDS and swizzle as nnGemm256, with the K-tile
+// cut into four phases (the HIP guide's phase-interleaved schedule).  A wave owns rows {64 wr + 0..63}
+// of both A halves (rows 0..127 | 128..255) and columns {32 wc + 0..31} of both B halves, so its
+// output is four 64 x 32 quadrants (Ah, Bh') and a phase computes one quadrant over K = 64 (16 MFMAs):
+//   p1 (A0, B0): read A0 sub-tile + B0 sub-tile; stage B1 of tile v+1 (other buffer)
+//   p2 (A0, B1): read B1;                         stage A1 of tile v+1 (other buffer)
+//   p3 (A1, B1): read A1;                         stage A0 of tile v+2 (this buffer: A0 last read in p1)
+//   p4 (A1, B0): no reads;                        stage B0 of tile v+2 (this buffer: B0 last read in p1);
+//                s_waitcnt vmcnt(4) retires tile v+1 (A0/B0 of v+2 stay in flight across the barrier)
+// Each phase: reads, stage, [wait], barrier, lgkmcnt(0), 16 MFMAs, barrier.  The wave group wr = 1 runs
+// one barrier behind group 0 (an extra barrier before the loop; group 0 takes it after), so on every
+// SIMD (one wave of each group) one wave issues MFMAs while the other reads LDS.  With that stagger a
+// half-tile is restaged at least two phases after its last read in either group, and a staged tile is
+// read one phase after the wait that retires it.
+// ---------------------------------------------------------------------------
+#ifndef NN8_STAGGER
+#define NN8_STAGGER 1  // wave group 1 one barrier behind group 0
+#endif
+#ifndef NN8_EARLY
+#define NN8_EARLY 0  // 1: both halves of tile v+1 still missing are staged in p1 (3 phases before the wait)
+#endif
+#ifndef NN8_PRIO_MODE
+#define NN8_PRIO_MODE 2  // 0: s_setprio(1) around each MFMA cluster; 1: once for group 1; 2: none (fastest, A/B)
+#endif
+#if NN8_PRIO_MODE == 0
+#define NN8_PRIO(x) __builtin_amdgcn_s_setprio(x)
+#else
+#define NN8_PRIO(x) ((void)0)
+#endif
+__global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
+    constexpr uint32_t T = 256, BK = 64, kOp = T * BK;
+    const int          lane = threadIdx.x & 63;
+    const uint32_t     wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t     nMT = a.Mpad / T, nNT = a.Npad / T, nwg = nMT * nNT;
+    const uint32_t     b = blockIdx.x, xcd = b & 7u, q = nwg / 8u, r = nwg % 8u;
+    const uint32_t     id = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (b >> 3);
+    const uint32_t     m0 = (id % nMT) * T, n0 = (id / nMT) * T;
+    const uint32_t     wr = wave >> 2, wc = wave & 3u;
+    const uint32_t     nK = a.Kpad / BK;
+
+    const auto stage = [&](int op, uint32_t h, uint32_t u, uint32_t buf) {
+        const uint16_t* src  = op == 0 ? a.A : a.B;
+        const uint32_t  base = op == 0 ? m0 : n0;
+#pragma unroll
+        for (uint32_t i = 0; i < 2; ++i) {
+            const uint32_t p   = wave * 128u + i * 64u + static_cast<uint32_t>(lane);
+            const uint32_t row = h * 128u + p / 8u;
+            const uint32_t c   = (p % 8u) ^ nnSwz(row);
+            __builtin_amdgcn_global_load_lds(src + static_cast<size_t>(base + row) * a.Kpad + u * BK + 8u * c,
+                                             nnLds + (buf * 2u + static_cast<uint32_t>(op)) * kOp + h * (kOp / 2) +
+                                                     (wave * 128u + i * 64u) * 8u,
+                                             16, 0, 0);
+        }
+    };
+    const auto frag = [&](uint32_t buf, int op, uint32_t row, uint32_t ks) {
+        const uint32_t c = ks * 4u + (static_cast<uint32_t>(lane) >> 4);
+        return *reinterpret_cast<const bf16x8*>(nnLds + (buf * 2u + static_cast<uint32_t>(op)) * kOp + row * BK +
+                                                (c ^ nnSwz(row)) * 8u);
+    };
+    const uint32_t rl = static_cast<uint32_t>(lane) & 15u;
+    // sub-tile reads: A half h -> rows 128 h + 64 wr + 16 i + rl; B half h -> rows 128 h + 32 wc + 16 j + rl
+    const auto readA = [&](uint32_t buf, uint32_t h, bf16x8(&fa)[4][2]) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa[i][ks] = frag(buf, 0, h * 128u + wr * 64u + 16u * i + rl, ks);
+    };
+    const auto readB = [&](uint32_t buf, uint32_t h, bf16x8(&fb)[2][2]) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                fb[j][ks] = frag(buf, 1, h * 128u + wc * 32u + 16u * j + rl, ks);
+    };
+
+    f32x4 acc[8][4];  // [4 ha + i][2 hb + j]
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const auto quadrant = [&](int ha, int hb, const bf16x8(&fa)[4][2], const bf16x8(&fb)[2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        NN8_PRIO(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[4 * ha + i][2 * hb + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[4 * ha + i][2 * hb + j], 0, 0, 0);
+        NN8_PRIO(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: tile 0 whole, A0 / B0 of tile 1; tile 0 retired
+    stage(0, 0, 0, 0);
+    stage(0, 1, 0, 0);
+    stage(1, 0, 0, 0);
+    stage(1, 1, 0, 0);
+    if (nK > 1) {
+        stage(0, 0, 1, 1);
+        stage(1, 0, 1, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (NN8_STAGGER && wr == 1)
+        __builtin_amdgcn_s_barrier();  // the stagger
+#if NN8_PRIO_MODE == 1
+    if (wr == 1)
+        __builtin_amdgcn_s_setprio(1);  // static form: the younger half keeps priority
+#endif
+
+    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+    for (uint32_t v = 0; v < nK; ++v) {
+        const uint32_t buf = v & 1u;
+        const bool     n1 = v + 1 < nK, n2 = v + 2 < nK;
+        // p1
+        readA(buf, 0, fa);
+        readB(buf, 0, fb0);
+        if (n1) {
+            stage(1, 1, v + 1, buf ^ 1u);
+            if (NN8_EARLY)
+                stage(0, 1, v + 1, buf ^ 1u);
+        }
+        __builtin_amdgcn_s_barrier();
+        quadrant(0, 0, fa, fb0);
+        __builtin_amdgcn_s_barrier();
+        // p2
+        readB(buf, 1, fb1);
+        if (!NN8_EARLY && n1)
+            stage(0, 1, v + 1, buf ^ 1u);
+        __builtin_amdgcn_s_barrier();
+        quadrant(0, 1, fa, fb1);
+        __builtin_amdgcn_s_barrier();
+        // p3
+        readA(buf, 1, fa);
+        if (n2)
+            stage(0, 0, v + 2, buf);
+        __builtin_amdgcn_s_barrier();
+        quadrant(1, 1, fa, fb1);
+        __builtin_amdgcn_s_barrier();
+        // p4
+        if (n2) {
+            stage(1, 0, v + 2, buf);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
+        else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        quadrant(1, 0, fa, fb0);
+        __builtin_amdgcn_s_barrier();
+    }
+    if (NN8_STAGGER && wr == 0)
+        __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+
+    // epilogue: rows m = m0 + 128 (i >> 2) + 64 wr + 16 (i & 3) + 4 (lane >> 4) + rr,
+    //           frame n = n0 + 128 (j >> 1) + 32 wc + 16 (j & 1) + (lane & 15)
+    const uint32_t g = static_cast<uint32_t>(lane) >> 4, col = rl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t mb = m0 + 128u * (i >> 2) + wr * 64u + 16u * (i & 3) + 4u * g;
+        const f32x4    bs = *reinterpret_cast<const f32x4*>(a.bias + mb);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t n = n0 + 128u * (j >> 1) + wc * 32u + 16u * (j & 1) + col;
+            if (a.top) {
+                if (n < a.nFrames)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        if (mb + rr < a.M)
+                            a.scores[static_cast<size_t>(mb + rr) * a.scoreStride + n] = -(acc[i][j][rr] + bs[rr]);
+            }
+            else {
+                u16x4 v;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    v[rr] = toBf16(activate(acc[i][j][rr] + bs[rr], a.act, a.gamma));
+                *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
+            }
+        }
+    }
+}
+
 }  // namespace dev
 
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
@@ -378,15 +570,20 @@ hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream) {
         return hipSuccess;
     if constexpr (kNnTileM == 256) {
         constexpr uint32_t kLds = 2u * 2u * 256u * 64u * 2u;  // 128 KiB
-        static bool        attr = false;
+#if NN_GEMM_VARIANT == 8
+        const auto kernel = dev::nnGemm8p;
+#else
+        const auto kernel = dev::nnGemm256;
+#endif
+        static bool attr = false;
         if (!attr) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::nnGemm256),
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLds));
             if (e != hipSuccess)
                 return e;
             attr = true;
         }
-        hipLaunchKernelGGL(dev::nnGemm256, dim3(nwg), dim3(512), kLds, stream, a);
+        hipLaunchKernelGGL(kernel, dim3(nwg), dim3(512), kLds, stream, a);
     }
     else {
         hipLaunchKernelGGL(dev::nnGemm, dim3(nwg), dim3(256), 0, stream, a);

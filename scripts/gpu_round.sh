@@ -19,7 +19,8 @@ step() {  # step <name> <timeout> <cmd...>
 STEPS=${STEPS:-"pytest smoke bench_fp32 bench_simd prof pmc"}
 for s in $STEPS; do
   case $s in
-    pytest) step pytest 1200 python -m pytest tests -x -q -m gpu ;;
+    pytest) step pytest 1200 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    bench) step bench 600 python bench.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_fp32) step bench_fp32 600 python bench.py --mode fp32 --steps 20 --warmup 3 ;;
     bench_simd) step bench_simd 600 python bench.py --mode simd --steps 20 --warmup 3 --cpu-baseline off ;;
