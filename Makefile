@@ -27,7 +27,7 @@ DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 REFSORT   = $(BUILD)/tests/refsort_test
 
-all: $(LIB) $(DRIVER) $(REFSORT) oracle
+all: $(LIB) $(DRIVER) $(REFSORT) oracle check-integration
 
 $(BUILD)/gmm_kernels_i8.o: $(SRC)/gmm_kernels_i8.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -100,8 +100,23 @@ $(DRIVER): tests/cpp/feature_scorer_driver.cc $(LIB) $(HDRS)
 oracle:
 	$(MAKE) -C oracle
 
+# The RASR-side adapter (integration/rasr/Mm/GpuFeatureScorer.{hh,cc}) compiled -fsyntax-only against the
+# reference's own headers with the reference's flags (config/cc-gcc.make:26-29).  Core/Utility.hh includes the
+# make-generated Modules.hh, so a one-line stand-in (MODULE_MM_BATCH, as src/Mm/Makefile:70-75 builds it) is
+# written under build/ for this check only; it pins no parity and nothing is linked.  Skipped where the
+# reference tree is absent (the GPU box).
+RASR_SRC ?= /root/reference/src
+check-integration: integration/rasr/Mm/GpuFeatureScorer.cc integration/rasr/Mm/GpuFeatureScorer.hh $(SRC)/host/GpuFeatureScorer.hh
+	@if [ -d "$(RASR_SRC)/Mm" ]; then \
+	    mkdir -p $(BUILD)/rasr_check && printf '#pragma once\n#define MODULE_MM_BATCH\n' > $(BUILD)/rasr_check/Modules.hh && \
+	    g++ -std=gnu++0x -fsyntax-only -funsigned-char -fno-exceptions -Wall -DPROC_x86_64 -DOS_linux \
+	        -DARCH_linux_x86_64 -D_GNU_SOURCE -I$(BUILD)/rasr_check -I$(RASR_SRC) -I/usr/include/libxml2 -Iinclude \
+	        -I$(SRC) integration/rasr/Mm/GpuFeatureScorer.cc && \
+	    echo "check-integration: adapter compiles against $(RASR_SRC)"; \
+	else echo "check-integration: $(RASR_SRC) absent, skipped"; fi
+
 clean:
 	rm -rf $(BUILD) $(LIBDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean check-integration

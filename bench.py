@@ -3,38 +3,49 @@
 
 Workload (BASELINE.json configs[1]): 800k-density triphone diag-GMM, 39-dim,
 5000 mixtures x 160 densities, pooled covariance, synthetic model and frames
-(SURVEY.md 8(d)); one step = scoring one batch of frames against every mixture
-(scores + best densities written to HBM), inputs resident in HBM.  Headline mode
-"fp32" is the diagonal-maximum scorer on f32 MFMA (configs[1] says fp32); the
-bit-exact SIMD-diagonal-maximum scorer (int8 MFMA) is timed too and reported
-under "modes".
+(SURVEY.md 8(d)); inputs resident in HBM.  One step scores a block of frames
+against every mixture (scores + best densities written to HBM): `--launches`
+scorer calls of `--frames` frames each (32768 by default), on consecutive frame
+slices into consecutive columns of one [mixtures][frames per step] table, so 20
+steps time >= 1 s of steady state (the loop is power-bound; a 0.1 s window reads
+the boost clock).  Headline mode "fp32" is the diagonal-maximum scorer
+(configs[1] says fp32); the bit-exact SIMD-diagonal-maximum scorer (int8 MFMA)
+is timed too and reported under "modes".
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fp32|simd] [--frames F]
-                  [--parallel frames|mixtures|densities]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fp32|simd|...] [--frames F]
+                  [--launches L] [--parallel frames|mixtures|densities]
 
-N > 1 is launched by torch.distributed.run, one process per GPU:
-  --parallel frames   (default; configs 2-3): every rank scores its own F frames
+--gpus N > 1 without WORLD_SIZE in the environment: this process starts
+`torch.distributed.run --nproc-per-node N bench.py ...` as a child (before any
+GPU call), relays its output and exits with its code; every rank checks that
+the world it joined has N ranks.  Layouts (one process per GPU, RCCL):
+  --parallel frames   (default; configs 2-3): every rank scores its own frames
                       against a replica of the model, no collective on the data
                       path, "scaling": "weak";
-  --parallel mixtures (config 4): every rank holds 1/N of the mixtures (density
-                      balanced) and scores the same F frames; the [M][F] score
-                      table is assembled with one all-gather over RCCL per step,
-                      "scaling": "strong";
+  --parallel mixtures: every rank holds 1/N of the mixtures (density balanced) and
+                      scores the same frames; the table is assembled with one
+                      all-gather per launch, "scaling": "strong";
   --parallel densities (config 4 as written): every rank holds 1/N of the densities
                       (mixtures on shard boundaries split between ranks) and scores
-                      the same F frames; whole mixtures all-gathered, split ones
+                      the same frames; whole mixtures all-gathered, split ones
                       reduced per frame with an RCCL all-reduce(MIN), "strong".
 A barrier + synchronize brackets the timed region; the max over ranks is reported.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP events
-on its stream) and the CPU baseline (oracle restatement of SIMD-diagonal-maximum
-on this host's cores, rank 0 at N=1 only).
+on its stream, averaged over every launch of the timed region), the CPU baseline
+(oracle restatements of SIMD-diagonal-maximum and diagonal-maximum on this host,
+rank 0 at N=1 only) and the host-buffer boundary rate (gmm_score_host into a
+page-locked table, PCIe included; never `value`).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -46,6 +57,7 @@ PEAK_F32_MFMA_TFLOPS = 157.3          # v_mfma_f32_16x16x4_f32, dense
 PEAK_F16_MFMA_TFLOPS = 2516.6         # v_mfma_f32_16x16x32_f16, dense (same rate as bf16)
 PEAK_I8_MFMA_TOPS = 2 * 2516.6        # i8 MFMA = 2x the bf16 dense rate
 SPLIT_PRODUCTS = 3                    # split-f16 kernel: mh*xh + mh*xl + ml*xh per f32 multiply-add
+CPU_SHARE_PER_GPU = 16                # host CPUs a one-GPU box grants this job
 
 MODES = {
     "fp32": ("diagonal-maximum", "f32"),
@@ -56,8 +68,9 @@ MODES = {
     "presel-float": ("preselection-batch-float", "f32"),
     "presel-int": ("preselection-batch-int", "s8xs8->i32 (u8-quantized, bit-exact)"),
 }
-DEFAULT_FRAMES = {"fp32": 32768, "simd": 32768, "sum": 32768, "nn": 32768, "presel-float": 32768,
-                  "presel-int": 32768}  # frames per GPU per step (batch)
+FRAMES_PER_LAUNCH = 32768  # frames per scorer call (the scorer's max_frames)
+# scorer calls per step: about 50-60 ms of GPU work per step at the measured rates, so 20 steps >= 1 s
+DEFAULT_LAUNCHES = {"fp32": 12, "simd": 24, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
 # BASELINE config 5 network (hybrid DNN): 11 x 39 spliced MFCC input, 6 sigmoid layers of 2048, 5000 classes
 NN_DIMS = [429] + [2048] * 6 + [5000]
 
@@ -68,7 +81,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--mode", choices=sorted(MODES), default="fp32")
-    p.add_argument("--frames", type=int, default=0, help="frames per GPU per step (default: mode-specific)")
+    p.add_argument("--frames", type=int, default=0, help=f"frames per scorer call (default {FRAMES_PER_LAUNCH})")
+    p.add_argument("--launches", type=int, default=0, help="scorer calls per step (default: mode-specific)")
     p.add_argument("--parallel", choices=["frames", "mixtures", "densities"], default="frames")
     p.add_argument("--mixtures", type=int, default=5000)
     p.add_argument("--densities", type=int, default=160)
@@ -78,12 +92,33 @@ def parse():
     p.add_argument("--native-f32", action="store_true",
                    help="fp32 mode on the f32-MFMA kernel instead of the split-f16 kernel")
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: the CPUs available)")
     p.add_argument("--cpu-frames-per-thread", type=int, default=3000)
+    p.add_argument("--host-boundary", choices=["auto", "off"], default="auto")
     return p.parse_args()
 
 
-def dist_setup():
+# ---------------------------------------------------------------------------
+# launcher: --gpus N without a torch.distributed environment
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Run this script as N ranks under torch.distributed.run (a child process; nothing here has touched the
+    GPU) and return its exit code.  The child's stdout (rank 0's JSON line) passes through unchanged."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dist_setup(args):
     """One process per GPU over RCCL ("nccl").  Rehearsal only (not used by the driver): with
     RASR_BENCH_SAME_DEVICE=1 every rank uses GPU 0 and RASR_BENCH_BACKEND=gloo replaces RCCL, so the
     N > 1 flow can be exercised on a one-GPU box."""
@@ -91,6 +126,8 @@ def dist_setup():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
     if os.environ.get("RASR_BENCH_SAME_DEVICE") == "1":
         local = 0
     if ws > 1:
@@ -101,6 +138,9 @@ def dist_setup():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        seen = dist.get_world_size()
+        if seen != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {seen} ranks")
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
@@ -124,49 +164,67 @@ def max_over_ranks(x: float, ws: int) -> float:
     return float(t.item())
 
 
-def load_pmc(mode: str):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (scripts/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE)."""
+def _library_sha() -> str:
+    from rasr_amd import _capi
+    h = hashlib.sha256()
+    with open(_capi.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def load_pmc(mode: str, frames_per_launch: int):
+    """HBM bytes per launch of the dominant kernel from the rocprofv3 PMC summary under profiles/
+    (scripts/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE), used only when it
+    was collected on this very library build and launch size; else null."""
     path = os.path.join(ROOT, "profiles", f"pmc_{mode}.json")
-    if not os.path.exists(path):
-        return None
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            pmc = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
+    if pmc.get("library_sha") != _library_sha() or pmc.get("frames_per_launch") != frames_per_launch:
+        return None, f"{os.path.relpath(path, ROOT)} is from another build or launch size"
+    return pmc.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
-def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
+def _step_slices(total: int, per: int):
+    return [(i, min(i + per, total)) for i in range(0, total, per)]
+
+
+def run_mode(args, mode, ms, ws, rank, local, launches):
     import torch
     import rasr_amd as ra
     from rasr_amd import parallel
     kind, dtype = MODES[mode]
     dev = torch.device("cuda", local)
+    fpl = args.frames or FRAMES_PER_LAUNCH
+    f_step = fpl * launches
     sharded = args.parallel in ("mixtures", "densities") and ws > 1
     if sharded:
         if args.parallel == "densities":
-            scorer = parallel.DensityShardedScorer(ms, kind, frames_per_gpu, rank, ws, device=local)
+            scorer = parallel.DensityShardedScorer(ms, kind, fpl, rank, ws, device=local)
         else:
-            scorer = parallel.MixtureShardedScorer(ms, kind, frames_per_gpu, rank, ws, device=local)
+            scorer = parallel.MixtureShardedScorer(ms, kind, fpl, rank, ws, device=local)
         sc = scorer.scorer
         seed = 1000  # every rank scores the same frames
     else:
-        sc = ra.Scorer(ms, kind, max_frames=frames_per_gpu, device=local,
-                       native_f32=args.native_f32 and mode == "fp32")
+        sc = ra.Scorer(ms, kind, max_frames=fpl, device=local, native_f32=args.native_f32 and mode == "fp32")
         seed = 1000 + rank
     m_local = sc.n_mixtures()
-    frames = torch.from_numpy(ra.synthetic_frames(frames_per_gpu, args.dim, seed=seed)).to(dev)
-    scores = torch.empty((m_local, frames_per_gpu), dtype=torch.float32, device=dev)
-    best = None if (args.no_best or mode.startswith("presel")) else torch.empty((m_local, frames_per_gpu), dtype=torch.int32,
-                                                                                   device=dev)
+    frames = torch.from_numpy(ra.synthetic_frames(f_step, args.dim, seed=seed)).to(dev)
+    want_best = not (args.no_best or mode.startswith("presel"))
+    scores = torch.empty((m_local, f_step if not sharded else fpl), dtype=torch.float32, device=dev)
+    best = (torch.empty((m_local, f_step if not sharded else fpl), dtype=torch.int32, device=dev)
+            if want_best else None)
     stream = torch.cuda.current_stream(dev)
+    slices = _step_slices(f_step, fpl)
 
     def step():
-        if sharded:
-            scorer.score(frames, scores, best, stream)  # score own mixtures + all-gather the table
-        else:
-            sc.score_device(frames, scores, best, stream)
+        for a, b in slices:
+            if sharded:  # this rank's mixtures / densities + the collectives, per launch
+                scorer.score(frames[a:b], scores, best, stream)
+            else:
+                sc.score_device(frames[a:b], scores[:, a:b], None if best is None else best[:, a:b], stream)
 
     for _ in range(args.warmup):
         step()
@@ -181,7 +239,7 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
     sc.set_timing(False)
     dt_max = max_over_ranks(dt, ws)
     kms_avg = max_over_ranks(kms / max(nl, 1), ws)
-    total_frames = (1 if sharded else ws) * frames_per_gpu * args.steps
+    total_frames = (1 if sharded else ws) * f_step * args.steps
     if sharded and args.parallel == "densities":
         d_local = scorer.shards[rank]["entries"][1] - scorer.shards[rank]["entries"][0]
     elif sharded:
@@ -189,7 +247,7 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
                       - ms.mixture_offsets[scorer.shards[rank][0]])
     else:
         d_local = int(ms.n_entries)
-    algo = 2.0 * args.dim * d_local * frames_per_gpu  # one multiply-add per (frame, density, component)
+    algo = 2.0 * args.dim * d_local * fpl  # one multiply-add per (frame, density, component), per launch
     kernel = sc.main_kernel()
     split = kernel in ("scoreSplit", "scoreSplit32", "scoreSplitSum")
     if split:
@@ -200,110 +258,197 @@ def run_mode(args, mode, ms, ws, rank, local, frames_per_gpu):
         peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PRODUCTS
         kq = 16 if kernel == "scoreSplit32" else 32
         k_issued = kq * ((3 * args.dim + 7 + kq - 1) // kq)
-        issued = 2.0 * k_issued * d_local * frames_per_gpu
+        issued = 2.0 * k_issued * d_local * fpl
     elif mode in ("fp32", "sum"):
         peak = PEAK_F32_MFMA_TFLOPS
-        issued = 2.0 * 4 * ((args.dim + 1 + 3) // 4) * d_local * frames_per_gpu
+        issued = 2.0 * 4 * ((args.dim + 1 + 3) // 4) * d_local * fpl
     else:
         peak = PEAK_I8_MFMA_TOPS
-        issued = 2.0 * 64 * ((args.dim + 63) // 64) * d_local * frames_per_gpu
+        issued = 2.0 * 64 * ((args.dim + 63) // 64) * d_local * fpl
     sec = kms_avg * 1e-3
     achieved = algo / sec / 1e12
+    traffic, traffic_src = load_pmc(mode, fpl) if not sharded else (None, None)
     res = {
         "value": total_frames / dt_max,
         "ms_per_step": dt_max / args.steps * 1e3,
         "dtype": dtype if not split else
         "f32 (operands split into 2 f16 pieces, 3 f16 MFMA products, f32 accumulate)",
-        "frames_per_gpu": frames_per_gpu,
+        "frames_per_step": f_step,
+        "frames_per_launch": fpl,
+        "launches_per_step": launches,
+        "timed_region_s": dt_max,
         "roofline": {
             "bound": "mfma",
             "achieved": achieved,
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": achieved / peak,
-            "traffic": load_pmc(mode) if not sharded else None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": kernel,
             "kernel_ms": kms_avg,
+            "kernel_launches_timed": nl,
             "algorithmic_flop_per_launch": algo,
             "issued_mfma_flop_per_launch": issued,
             "issued_mfma_tflops": issued / sec / 1e12,
             "issued_mfma_frac_of_dtype_peak": issued / sec / 1e12 / (
                 PEAK_F16_MFMA_TFLOPS if split else peak),
-            "output_bytes_per_launch": m_local * frames_per_gpu * (4 + (0 if best is None else 4)),
+            "output_bytes_per_launch": m_local * fpl * (4 + (0 if best is None else 4)),
         },
     }
-    del sc
+    del sc, scores, best, frames
+    torch.cuda.empty_cache()
     return res
 
 
-def run_nn(args, ws, rank, local, frames_per_gpu):
+def run_nn(args, ws, rank, local, launches):
     """Nn::BatchFeatureScorer drop-in (rasr_amd.nn): one bf16 MFMA GEMM per layer, bias + activation fused;
-    a step scores frames_per_gpu frames on every rank (frame-sharded replicas, no collective)."""
+    a step scores launches x frames on every rank (frame-sharded replicas, no collective)."""
     import numpy as np
     import torch
     import rasr_amd as ra
     from rasr_amd import nn
     dev = torch.device("cuda", local)
+    fpl = args.frames or FRAMES_PER_LAUNCH
+    f_step = fpl * launches
     layers = nn.synthetic_network(NN_DIMS, "sigmoid", seed=2024)
     lp = np.full(NN_DIMS[-1], -np.log(NN_DIMS[-1]), np.float32)
-    sc = nn.NnScorer(layers, log_prior=lp, prior_scale=1.0, max_frames=frames_per_gpu, device=local)
-    frames = torch.from_numpy(ra.synthetic_frames(frames_per_gpu, NN_DIMS[0], seed=1000 + rank)).to(dev)
-    scores = torch.empty((NN_DIMS[-1], frames_per_gpu), dtype=torch.float32, device=dev)
+    sc = nn.NnScorer(layers, log_prior=lp, prior_scale=1.0, max_frames=fpl, device=local)
+    frames = torch.from_numpy(ra.synthetic_frames(f_step, NN_DIMS[0], seed=1000 + rank)).to(dev)
+    scores = torch.empty((NN_DIMS[-1], f_step), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    slices = _step_slices(f_step, fpl)
+
+    def step():
+        for a, b in slices:
+            sc.score_device(frames[a:b], scores[:, a:b], stream)
+
     for _ in range(args.warmup):
-        sc.score_device(frames, scores, stream)
+        step()
     barrier(ws)
     sc.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sc.score_device(frames, scores, stream)
+        step()
     barrier(ws)
     dt = time.perf_counter() - t0
     kms, nl = sc.kernel_time(reset=True)
     sc.set_timing(False)
     dt_max = max_over_ranks(dt, ws)
     kms_avg = max_over_ranks(kms / max(nl, 1), ws)
-    algo = 2.0 * sum(a * b for a, b in zip(NN_DIMS[:-1], NN_DIMS[1:])) * frames_per_gpu
-    pad = lambda x, q: (x + q - 1) // q * q  # GEMM tiles: outputs to 128, the input to 64
-    kp = [pad(NN_DIMS[0], 64)] + [pad(d, 128) for d in NN_DIMS[1:-1]]
-    issued = 2.0 * sum(k * pad(m, 128) for k, m in zip(kp, NN_DIMS[1:])) * pad(frames_per_gpu, 128)
+    algo = 2.0 * sum(a * b for a, b in zip(NN_DIMS[:-1], NN_DIMS[1:])) * fpl
+    pad = lambda x, q: (x + q - 1) // q * q  # GEMM tiles: outputs to 256, the input to 64
+    kp = [pad(NN_DIMS[0], 64)] + [pad(d, 256) for d in NN_DIMS[1:-1]]
+    issued = 2.0 * sum(k * pad(m, 256) for k, m in zip(kp, NN_DIMS[1:])) * pad(fpl, 256)
     sec = kms_avg * 1e-3
     return {
-        "value": ws * frames_per_gpu * args.steps / dt_max,
+        "value": ws * f_step * args.steps / dt_max,
         "ms_per_step": dt_max / args.steps * 1e3,
         "dtype": MODES["nn"][1],
-        "frames_per_gpu": frames_per_gpu,
+        "frames_per_step": f_step,
+        "frames_per_launch": fpl,
+        "launches_per_step": launches,
+        "timed_region_s": dt_max,
         "roofline": {
             "bound": "mfma", "achieved": algo / sec / 1e12, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": algo / sec / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None, "kernel": "nnGemm8p",
+            "frac": algo / sec / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None, "kernel": "nnGemm8p (all layers)",
             "kernel_ms": kms_avg, "algorithmic_flop_per_launch": algo, "issued_mfma_flop_per_launch": issued,
             "issued_mfma_tflops": issued / sec / 1e12,
         },
     }
 
 
+# ---------------------------------------------------------------------------
+# CPU baseline and host boundary (rank 0, N = 1)
+# ---------------------------------------------------------------------------
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def available_cpus():
+    """(threads to use, note): the CPUs this process may run on -- affinity, capped by a cgroup CPU quota and by
+    the per-GPU CPU share of the GPU box (CPU_SHARE_PER_GPU; os.cpu_count() reports the whole machine there)."""
+    n = len(os.sched_getaffinity(0))
+    note = f"{n} CPUs in the affinity mask"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(p)))
+            if quota < n:
+                n, note = quota, f"cgroup quota {quota} CPUs"
+    except (OSError, ValueError):
+        pass
+    if n > CPU_SHARE_PER_GPU:
+        n, note = CPU_SHARE_PER_GPU, f"capped at the box's per-GPU CPU share ({note})"
+    return n, note
+
+
 def cpu_baseline(args, ms):
     import oracle
     import rasr_amd as ra
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    n = threads * args.cpu_frames_per_thread
-    frames = ra.synthetic_frames(n, args.dim, seed=999)
-    o = oracle.OracleSimd(ms)
+    threads, note = (args.cpu_threads, "--cpu-threads") if args.cpu_threads else available_cpus()
+    out = {}
+    for name, per_thread in (("SIMD-diagonal-maximum", args.cpu_frames_per_thread),
+                             ("diagonal-maximum", max(1, args.cpu_frames_per_thread // 2))):
+        n = threads * per_thread
+        frames = ra.synthetic_frames(n, args.dim, seed=999)
+        o = oracle.OracleSimd(ms) if name.startswith("SIMD") else oracle.OracleFloat(ms)
+        t0 = time.perf_counter()
+        o.score(frames, n_threads=threads)
+        dt = time.perf_counter() - t0
+        out[name] = {"value": n / dt, "frames": n, "seconds": dt}
+        del o
+    simd, flt = out["SIMD-diagonal-maximum"], out["diagonal-maximum"]
+    return {"value": flt["value"], "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": (f"{flt['frames']} frames x {ms.n_entries} densities, diagonal-maximum restatement "
+                       f"(oracle/gmm_oracle.c orc_float_score, SSE3 distance in the reference's order), {threads} "
+                       f"threads, {flt['seconds']:.1f} s; SIMD-diagonal-maximum restatement (SSE2 u8 SSD like the "
+                       f"reference JIT): {simd['frames']} frames, {simd['seconds']:.1f} s"),
+            "cpu_model": _cpu_model(), "host_logical_cpus": os.cpu_count(), "threads_note": note,
+            "modes": {"diagonal-maximum": flt["value"], "SIMD-diagonal-maximum": simd["value"]}}
+
+
+def host_boundary(args, ms, kind, calls=6):
+    """gmm_score_host (host frames in, host score + best tables out, PCIe included) into page-locked tables
+    (rasr_amd.pinned_empty = gmm_host_alloc), the path an RASR caller reading score(e) on the host takes."""
+    import rasr_amd as ra
+    fpl = args.frames or FRAMES_PER_LAUNCH
+    sc = ra.Scorer(ms, kind, max_frames=fpl)
+    frames = ra.synthetic_frames(fpl, args.dim, seed=555)
+    out = ra.pinned_empty((sc.n_mixtures(), fpl), "float32")
+    best = ra.pinned_empty((sc.n_mixtures(), fpl), "uint32")
+    sc.score_host(frames, out=out, best_out=best)  # warm-up (pipeline streams, staging)
     t0 = time.perf_counter()
-    o.score(frames, n_threads=threads)
+    for _ in range(calls):
+        sc.score_host(frames, out=out, best_out=best)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames x {ms.n_entries} densities, SIMD-diagonal-maximum restatement "
-                      f"(oracle/gmm_oracle.c, SSE2 u8 SSD like the reference JIT), {threads} threads, {dt:.1f} s"}
+    sc.close()
+    return {"value": calls * fpl / dt, "unit": "frames/s", "scorer": kind, "frames_per_call": fpl,
+            "path": "gmm_score_host, pinned score + best tables (gmm_host_alloc), PCIe-inclusive; not `value`",
+            "d2h_gb_per_s": calls * fpl * ms.n_mixtures * 8 / dt / 1e9}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if os.environ.get("RASR_BENCH_LAUNCH_PROBE") == "1":  # tests/test_bench_launcher.py: the ranks, no GPU work
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "gpus": args.gpus}), flush=True)
+        return
     import rasr_amd as ra
-    ws, rank, local = dist_setup()
-    frames_per_gpu = args.frames or DEFAULT_FRAMES[args.mode]
+    ws, rank, local = dist_setup(args)
+    launches = args.launches or DEFAULT_LAUNCHES[args.mode]
     if args.mode == "nn":
-        res = run_nn(args, ws, rank, local, frames_per_gpu)
+        res = run_nn(args, ws, rank, local, launches)
         if rank == 0:
             print(json.dumps({
                 "metric": "frames/sec scored, hybrid-DNN posteriors (Nn::BatchFeatureScorer)", "value": res["value"],
@@ -311,23 +456,29 @@ def main():
                 "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": res["dtype"], "data": "synthetic (random-init network, frames N(0,1))",
                 "config": {"workload": "hybrid DNN " + "-".join(map(str, NN_DIMS)) + " sigmoid, 5000 classes",
-                           "frames_per_gpu_per_step": frames_per_gpu,
+                           "frames_per_gpu_per_step": res["frames_per_step"],
+                           "frames_per_launch": res["frames_per_launch"],
                            "parallelism": f"frame-sharded replicas x{ws}"},
-                "roofline": res["roofline"], "cpu_baseline": None}), flush=True)
+                "timed_region_s": res["timed_region_s"], "roofline": res["roofline"], "cpu_baseline": None}),
+                flush=True)
         if ws > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
         return
     ms = ra.synthetic_mixture_set(args.mixtures, args.densities, args.dim, seed=2024)
-    res = run_mode(args, args.mode, ms, ws, rank, local, frames_per_gpu)
+    res = run_mode(args, args.mode, ms, ws, rank, local, launches)
     extra = {}
     if not args.no_extra_mode:
         other = "simd" if args.mode != "simd" else "fp32"  # (nn returned above)
-        r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_FRAMES[other])
+        r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_LAUNCHES[other])
         extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
-                        "frames_per_gpu_per_step": r2["frames_per_gpu"], "dtype": r2["dtype"],
+                        "frames_per_gpu_per_step": r2["frames_per_step"], "frames_per_launch": r2["frames_per_launch"],
+                        "timed_region_s": r2["timed_region_s"], "dtype": r2["dtype"],
                         "scorer": MODES[other][0], "roofline": r2["roofline"]}
     cpu = None
+    hb = None
+    if rank == 0 and ws == 1 and args.host_boundary == "auto" and not args.mode.startswith("presel"):
+        hb = host_boundary(args, ms, MODES[args.mode][0])
     if rank == 0 and ws == 1 and args.cpu_baseline == "auto":
         cpu = cpu_baseline(args, ms)
     if rank == 0:
@@ -352,14 +503,17 @@ def main():
                 "mixtures": args.mixtures,
                 "densities_per_mixture": args.densities,
                 "dimension": args.dim,
-                "frames_per_gpu_per_step": frames_per_gpu,
+                "frames_per_gpu_per_step": res["frames_per_step"],
+                "frames_per_launch": res["frames_per_launch"],
                 "best_density": not args.no_best and not args.mode.startswith("presel"),
                 "parallelism": (f"mixture-sharded x{ws} + RCCL all-gather" if args.parallel == "mixtures" and ws > 1
                                 else f"density-sharded x{ws} + RCCL all-reduce(MIN) of split mixtures + all-gather"
                                 if args.parallel == "densities" and ws > 1 else f"frame-sharded replicas x{ws}"),
             },
+            "timed_region_s": res["timed_region_s"],
             "roofline": res["roofline"],
             "cpu_baseline": cpu,
+            "host_boundary": hb,
         }
         if extra:
             line["modes"] = extra

@@ -240,6 +240,41 @@ def batch_float_score(ms, frames, n_threads: int = 1):
     return scores
 
 
+def batch_fast_score(ms, frames):
+    """batch-diagonal-maximum-fast restated: BatchUnrolledIntFeatureScorer::fillScoreCache
+    (src/Mm/BatchFeatureScorer.cc:558-604) over BatchIntFeatureScorer::init's tables (cc:339-380).  The
+    unrolled loop always loads 3 x 16 feature bytes and 3 x 16 mean bytes and advances the mean pointer by
+    the fixed 48 bytes (`mean += Dimension`, cc:591), while init lays the means out at paddedDimension_
+    (cc:367-375).  For a padded dimension of 48 (dimension 33..48) that is batch-int's arithmetic; for 16
+    or 32 the loads run into the next buffered features and the next densities' means, and the last
+    mixture's past the end of the allocation (cc:362-363), so the reference result is undefined there and
+    this restatement refuses, as the GPU scorer does."""
+    d = _Desc(ms)
+    D = ms.means.shape[1]
+    dp = (D + 15) // 16 * 16
+    if dp != 48:
+        raise ValueError(f"padded dimension {dp}: the reference's unrolled loads leave its own rows")
+    scale, _, const = batch_int_prepare(ms)
+    var = np.empty(dp, np.float32)
+    means = np.empty((d.n_entries, dp), np.uint8)
+    if load().orc_batch_int_tables(ctypes.byref(d.c), var.ctypes.data_as(_vp), means.ctypes.data_as(_vp)) != 0:
+        raise ValueError("orc_batch_int_tables failed")
+    f, n, _ = _frames(frames)
+    feats = np.zeros((n, dp), np.uint8)
+    feats[:, :D] = quantize_array(f * var[:D]).reshape(n, D)  # setFeature: q(f * variance_) (cc:382-388)
+    off = d.mo.astype(np.int64)
+    scores = np.empty((d.n_mixtures, n), np.float32)
+    for m in range(d.n_mixtures):
+        mm = means[off[m]:off[m + 1]].reshape(-1, 48).astype(np.int32)  # the 48-byte stride of cc:591
+        best = np.full(n, 2147483647, np.int64)
+        if mm.shape[0]:
+            dist = ((feats[:, None, :].astype(np.int32) - mm[None]) ** 2).sum(-1)  # addDistance x 3 blocks
+            tmp = dist + const[off[m]:off[m + 1]][None].astype(np.int64)
+            best = np.minimum(best, tmp.min(1))  # strict < from INT_MAX (cc:593-597)
+        scores[m] = best.astype(np.int32).astype(np.float32) / np.float32(scale)  # (f32)best / scale_ (cc:602)
+    return scores
+
+
 def inverse_sqrt(x: float) -> float:
     return load().orc_inverse_sqrt(x)
 

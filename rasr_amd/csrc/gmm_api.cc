@@ -103,6 +103,7 @@ struct gmm_scorer {
     uint32_t* dRowDns    = nullptr;
     uint32_t* dMixTileOff = nullptr;
     float*    dIsv       = nullptr;
+    float*    dCentre    = nullptr;  // float types: centre of the expanded quadratic form [D]
     // device frame staging
     int8_t*  dFrameQ  = nullptr;
     int32_t* dFrameSS = nullptr;
@@ -134,7 +135,7 @@ struct gmm_scorer {
     ~gmm_scorer() {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
                         dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
-                        dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu};
+                        dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu, dCentre};
         for (void* p : ptrs)
             if (p)
                 (void)hipFree(p);
@@ -296,7 +297,7 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
     }
     else if (s->split) {
         GMM_HIP_CHECK(launchPrepareFramesSplit(frames, nFrames, frameStride, nPadCall, s->D, s->splitRows, s->kSteps16, s->dIsv,
-                                               s->dDimScale, s->dLimbExp, s->dFrameH, s->dFrameXX, s->dFrameExp,
+                                               s->dCentre, s->dDimScale, s->dLimbExp, s->dFrameH, s->dFrameXX, s->dFrameExp,
                                                stream));
         SplitArgs a{};
         a.tileH       = s->dTileA;
@@ -332,7 +333,8 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
     }
     else {
         GMM_HIP_CHECK(launchPrepareFramesF32(frames, nFrames, frameStride, s->nFramesPad, nPadCall, s->D, s->C, s->kSteps,
-                                             s->foldNorm ? 1 : 0, s->dIsv, s->dFrameX, s->dFrameXX, stream));
+                                             s->foldNorm ? 1 : 0, s->dIsv, s->dCentre, s->dFrameX, s->dFrameXX,
+                                             stream));
         F32Args a{};
         a.tileA       = static_cast<const float*>(s->dTileA);
         a.tileCov     = s->dTileCov;
@@ -476,8 +478,8 @@ int ensureHostStage(gmm_scorer* s, size_t rowBytes) {
     return GMM_OK;
 }
 
-int scoreHostPipelined(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
-                       uint32_t* best, uint32_t scoreStride) {
+int scoreHostPipelinedImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+                           uint32_t* best, uint32_t scoreStride) {
     const uint32_t fpb = framesPerBlock(s);
     // one chunk for preselection: gmm_scorer_cluster_selection reports the last call's whole batch
     uint32_t nChunks = s->presel ? 1u : std::clamp<uint32_t>(nFrames / kHostChunkFrames, 1u, kHostMaxChunks);
@@ -566,6 +568,19 @@ int scoreHostPipelined(gmm_scorer* s, const float* frames, uint32_t nFrames, uin
     return GMM_OK;
 }
 
+// On an error after work was queued, wait for both pipeline streams before returning: no DMA into the
+// caller's buffers and no kernel reading dHostFrames may outlive the call (later calls order only against
+// the null stream).
+int scoreHostPipelined(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+                       uint32_t* best, uint32_t scoreStride) {
+    const int rc = scoreHostPipelinedImpl(s, frames, nFrames, frameStride, scores, best, scoreStride);
+    if (rc != GMM_OK)
+        for (hipStream_t st : {s->hostCompute, s->hostCopy})
+            if (st)
+                (void)hipStreamSynchronize(st);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -585,8 +600,16 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         cfg = *config;
     if (cfg.max_frames == 0)
         return fail(GMM_ERR_INVALID_ARGUMENT, "max_frames must be > 0");
+    // BatchUnrolledIntFeatureScorer (BatchFeatureScorer.cc:550-604): padded dimension > 48 is refused by the
+    // reference itself (cc:552-555); below 48 its unrolled loop still loads 3 x 16 bytes per row and steps the
+    // means by 48 bytes (cc:591) across rows laid out at the padded dimension (cc:367-375), reading other rows
+    // and past its allocation -- undefined, so refused here; at exactly 48 it is batch-int's arithmetic.
     if (type == GMM_BATCH_DIAGONAL_MAXIMUM_FAST && (ms->dimension + 15) / 16 * 16 > 48)
         return fail(GMM_ERR_UNSUPPORTED, "This feature scorer supports only features with max. 48 components");
+    if (type == GMM_BATCH_DIAGONAL_MAXIMUM_FAST && (ms->dimension + 15) / 16 * 16 < 48)
+        return fail(GMM_ERR_UNSUPPORTED, "batch-diagonal-maximum-fast needs 33..48 components (padded dimension 48): "
+                                         "the reference's fixed 48-byte loads are undefined for smaller dimensions; "
+                                         "use batch-diagonal-maximum-int");
     const bool presel = type == GMM_BATCH_PRESELECTION_FLOAT || type == GMM_BATCH_PRESELECTION_INT;
     if (presel && (cfg.clusters == 0 || cfg.clusters > 256))
         return fail(GMM_ERR_INVALID_ARGUMENT, "clusters must be in [1, 256]");
@@ -682,7 +705,8 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
             const size_t nH = static_cast<size_t>(s->nFramesPad) * p.kSteps16 * (p.splitRows == 32 ? 16 : 32);
             if ((rc = upload(reinterpret_cast<uint16_t**>(&s->dTileA), p.tileH, kTilePad * kLanes * 8 * p.kSteps16)) ||
                 (rc = upload(&s->dDimScale, p.dimScale)) || (rc = upload(&s->dLimbExp, limbs)) ||
-                (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)))
+                (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)) ||
+                (rc = upload(&s->dCentre, p.centre)))
                 return rc;
             GMM_HIP_CHECK(hipMalloc(&s->dFrameH, nH * sizeof(uint16_t)));
             GMM_HIP_CHECK(hipMemset(s->dFrameH, 0, nH * sizeof(uint16_t)));
@@ -712,7 +736,8 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         if ((rc = upload(reinterpret_cast<float**>(&s->dTileA), p.tileA, kTilePad * kLanes * p.kSteps)) ||
             (rc = upload(&s->dTileCov, p.tiling.tileCovariance, kTilePad)) ||
             (rc = upload(&s->dRowDns, p.tiling.rowDensityInMixture, kTilePad * kTileRows)) ||
-            (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)))
+            (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = upload(&s->dIsv, p.isvDevice)) ||
+            (rc = upload(&s->dCentre, p.centre)))
             return rc;
         const size_t nX = static_cast<size_t>(s->C) * s->nFramesPad;
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameX), nX * s->kSteps * 4 * sizeof(float)));

@@ -111,10 +111,12 @@ hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t
                                  uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, const float* isv, int8_t* frameQ,
                                  int32_t* frameSS, hipStream_t stream);
 hipError_t launchPrepareFramesF32(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
-                                  uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, int foldNorm, const float* isv, float* frameX,
+                                  uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, int foldNorm, const float* isv,
+                                  const float* centre, float* frameX,
                                   float* frameXX, hipStream_t stream);
 hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
-                                    uint32_t D, uint32_t rows, uint32_t kSteps, const float* isv, const float* dimScale,
+                                    uint32_t D, uint32_t rows, uint32_t kSteps, const float* isv, const float* centre,
+                                    const float* dimScale,
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream);
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps, hipStream_t stream);

@@ -41,7 +41,8 @@ __global__ __launch_bounds__(256) void prepareFramesF32(const float* __restrict_
                                                          uint32_t frameStride, uint32_t nFramesPad,
                                                          uint32_t nFramesRead, uint32_t D,
                                                          uint32_t C, uint32_t KS, int foldNorm,
-                                                         const float* __restrict__ isv, float* __restrict__ frameX,
+                                                         const float* __restrict__ isv,
+                                                         const float* __restrict__ centre, float* __restrict__ frameX,
                                                          float* __restrict__ frameXX) {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= C * nFramesRead)
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(256) void prepareFramesF32(const float* __restrict_
     float          xx    = 0.0f;
     if (valid)
         for (uint32_t k = 0; k < D; ++k) {
-            const float v = __fmul_rn(x[k], iv[k]);
+            const float v = __fmul_rn(__fsub_rn(x[k], centre[k]), iv[k]);
             xx            = __fadd_rn(xx, __fmul_rn(v, v));
         }
     float* base = frameX + (static_cast<size_t>(c) * (nFramesPad / 16) + f / 16) * KS * 64;
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(256) void prepareFramesF32(const float* __restrict_
         float v = 0.0f;
         if (valid) {
             if (k < D)
-                v = __fmul_rn(x[k], iv[k]);
+                v = __fmul_rn(__fsub_rn(x[k], centre[k]), iv[k]);
             else if (k == D)
                 v = 1.0f;
             else if (k == D + 1 && foldNorm)
@@ -323,10 +324,11 @@ using dev::prepareFramesF32;
 
 hipError_t launchPrepareFramesF32(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
                                   uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, int foldNorm,
-                                  const float* isv, float* frameX, float* frameXX, hipStream_t stream) {
+                                  const float* isv, const float* centre, float* frameX, float* frameXX,
+                                  hipStream_t stream) {
     const uint32_t n = C * nFramesRead;
     hipLaunchKernelGGL(prepareFramesF32, dim3((n + 255) / 256), dim3(256), 0, stream, frames, nFrames, frameStride,
-                       nFramesPad, nFramesRead, D, C, KS, foldNorm, isv, frameX, frameXX);
+                       nFramesPad, nFramesRead, D, C, KS, foldNorm, isv, centre, frameX, frameXX);
     return hipGetLastError();
 }
 

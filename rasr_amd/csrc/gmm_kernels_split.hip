@@ -67,6 +67,7 @@ template <int ROWS>
 __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restrict__ frames, uint32_t nFrames,
                                                            uint32_t frameStride, uint32_t nFramesRead, uint32_t D,
                                                            uint32_t KS16, const float* __restrict__ isv,
+                                                           const float* __restrict__ centre,
                                                            const float* __restrict__ dimScale,
                                                            const int32_t* __restrict__ limbExp,
                                                            u32x4* __restrict__ frameH, float* __restrict__ frameXX,
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
     bool         finite = true;
     if (valid)
         for (uint32_t k = 0; k < D; ++k) {
-            const float v = __fmul_rn(x[k], isv[k]);  // x' exactly as the f32 kernel forms it
+            const float v = __fmul_rn(__fsub_rn(x[k], centre[k]), isv[k]);  // x' as the f32 kernel forms it
             xx            = __fadd_rn(xx, __fmul_rn(v, v));
             const float y = fabsf(v * dimScale[k]);
             finite        = finite && y <= 3.40282347e+38f;
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
                 uint16_t       h = 0;
                 if (k < 3 * D) {
                     const uint32_t d  = k < D ? k : (k < 2 * D ? k - D : k - 2 * D);
-                    const float    y  = ldexpf(__fmul_rn(x[d], isv[d]) * dimScale[d], -e);
+                    const float    y  = ldexpf(__fmul_rn(__fsub_rn(x[d], centre[d]), isv[d]) * dimScale[d], -e);
                     const uint16_t hi = h16bits(y);
                     h = (k >= D && k < 2 * D) ? h16bits(y - static_cast<float>(__builtin_bit_cast(_Float16, hi))) : hi;
                 }
@@ -862,16 +863,17 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
 }  // namespace dev
 
 hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
-                                    uint32_t D, uint32_t rows, uint32_t kSteps, const float* isv, const float* dimScale,
+                                    uint32_t D, uint32_t rows, uint32_t kSteps, const float* isv, const float* centre,
+                                    const float* dimScale,
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream) {
     if (rows == 32)
         hipLaunchKernelGGL(dev::prepareFramesSplit<32>, dim3((nFramesRead + 255) / 256), dim3(256), 0, stream, frames,
-                           nFrames, frameStride, nFramesRead, D, kSteps, isv, dimScale, limbExp,
+                           nFrames, frameStride, nFramesRead, D, kSteps, isv, centre, dimScale, limbExp,
                            static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
     else
         hipLaunchKernelGGL(dev::prepareFramesSplit<16>, dim3((nFramesRead + 255) / 256), dim3(256), 0, stream, frames,
-                           nFrames, frameStride, nFramesRead, D, kSteps, isv, dimScale, limbExp,
+                           nFrames, frameStride, nFramesRead, D, kSteps, isv, centre, dimScale, limbExp,
                            static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
     return hipGetLastError();
 }

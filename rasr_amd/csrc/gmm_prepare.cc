@@ -354,6 +354,18 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
         out.logNorm[c] = dm ? ln * (gs * gs) : ln;
     }
 
+    // centre of the expansion: the mean over all means of the set (not only the shard's, so every
+    // shard of a model takes the same one)
+    out.centre.assign(D, 0.0f);
+    if (ms.n_means > 0)
+        for (uint32_t k = 0; k < D; ++k) {
+            double sum = 0;
+            for (uint32_t i = 0; i < ms.n_means; ++i)
+                sum += ms.means[static_cast<size_t>(i) * D + k];
+            const float c = static_cast<float>(sum / ms.n_means);
+            out.centre[k] = std::isfinite(c) ? c : 0.0f;
+        }
+
     buildTiling(ms, shard, out.tiling);
     const uint32_t T = out.tiling.nTiles, KS = out.kSteps;
 
@@ -400,7 +412,9 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
         const float*   iv   = out.isv.data() + static_cast<size_t>(cov) * D;
         double         mm   = 0;
         for (uint32_t k = 0; k < D; ++k) {
-            const float mp = mean[k] * iv[k];
+            // (mu - c) isv in f64, one rounding to the f32 operand; the reference's own difference is
+            // (mu - x) isv in f32 (GaussDiagonalMaximumFeatureScorer.cc:144-218)
+            const float mp = static_cast<float>((static_cast<double>(mean[k]) - out.centre[k]) * iv[k]);
             m2[k]          = -2.0f * mp;
             mm += static_cast<double>(mp) * mp;
         }

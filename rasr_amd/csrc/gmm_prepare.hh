@@ -91,6 +91,10 @@ struct PreparedFloat {
     Tiling             tiling;
     std::vector<float> tileA;         // [nTiles][kSteps][64 lanes]  (empty when split)
     std::vector<float> isvDevice;     // [C][kSteps*4] zero padded
+    // per-dimension centre (input units, the mean of all the set's means): both sides of the
+    // expanded quadratic form are taken about it, x' = (x - c) isv, m' = (mu - c) isv, so the
+    // terms ||x'||^2, ||m'||^2, x'.m' stay of the order of the model's spread, not of |mu / sigma|
+    std::vector<float> centre;        // [dimension]
     std::vector<uint32_t> splitFillEntry; // split tiling: [tile] the entry its padding rows repeat
     // split-f16 kernel (single covariance, gmm_kernels_split.hip): every f32 operand is a sum of
     // two f16 pieces, hi + lo; a row is  sum_d [mh*xh + mh*xl + ml*xh]  +  sum_s limb_s * 2^(b_s)

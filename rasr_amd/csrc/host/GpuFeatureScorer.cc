@@ -2,10 +2,32 @@
 #include "GpuFeatureScorer.hh"
 
 #include <cassert>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace Mm {
 namespace Gpu {
+
+namespace {
+void abortHandler(const std::string& message) {
+    std::fprintf(stderr, "criticalError: GPU feature scorer: %s\n", message.c_str());
+    std::fflush(stderr);
+    std::abort();
+}
+CriticalErrorHandler gCriticalError = abortHandler;
+
+[[noreturn]] void criticalError(const char* what) {
+    gCriticalError(std::string(what) + ": " + gmm_last_error());
+    std::abort();  // a handler that returns normally must not continue with missing scores
+}
+}  // namespace
+
+CriticalErrorHandler setCriticalErrorHandler(CriticalErrorHandler handler) {
+    CriticalErrorHandler prev = gCriticalError;
+    gCriticalError            = handler ? handler : abortHandler;
+    return prev;
+}
 
 // ---------------------------------------------------------------------------
 // MixtureSet
@@ -221,7 +243,7 @@ Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
     std::vector<float>    s(nMixtures_);
     std::vector<uint32_t> b(nMixtures_);
     if (gmm_score_host(handle_, f.data(), 1, dimension_, s.data(), assigning_ ? b.data() : nullptr, 1) != GMM_OK)
-        return Scorer();
+        criticalError("gmm_score_host");
     return std::make_shared<FrameScorer>(std::move(s), std::move(b), assigning_);
 }
 
@@ -236,12 +258,13 @@ std::unique_ptr<GpuBatchFeatureScorer> GpuBatchFeatureScorer::create(const Mixtu
         return nullptr;
     s->bufferSize_ = b;
     s->features_.assign(static_cast<size_t>(b) * s->dimension_, 0.0f);
-    s->scores_.assign(static_cast<size_t>(s->nMixtures_) * b, 0.0f);
-    s->best_.assign(static_cast<size_t>(s->nMixtures_) * b, 0xffffffffu);
+    const size_t n = std::max<size_t>(1, static_cast<size_t>(s->nMixtures_) * b);
+    if (!s->scores_.allocate(n, 0.0f) || (s->assigning_ && !s->best_.allocate(n, 0xffffffffu))) {
+        if (error)
+            *error = gmm_last_error();
+        return nullptr;
+    }
     s->cached_.assign(b, 0);
-    s->gather_.resize(static_cast<size_t>(b) * s->dimension_);
-    s->gatherScores_.resize(static_cast<size_t>(s->nMixtures_) * b);
-    s->gatherBest_.resize(static_cast<size_t>(s->nMixtures_) * b);
     return s;
 }
 
@@ -289,28 +312,23 @@ Scorer GpuBatchFeatureScorer::flush() const {
 }
 
 // Score all mixtures of the buffered positions featureIndex .. featureIndex+length-1 (mod buffer)
-// in one launch and cache them (the reference's fillScoreCache does one mixture at a time).
+// and cache them (the reference's fillScoreCache does one mixture at a time).  The positions form at
+// most two contiguous runs of the ring; each run is one gmm_score_host call that reads its rows of
+// features_ and writes its columns of the page-locked [nMixtures][bufferSize] tables in place.
 void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
     const uint32_t b = bufferSize_;
     length           = std::min(length, b);
-    for (uint32_t i = 0; i < length; ++i) {
-        const uint32_t p = (featureIndex + i) % b;
-        std::copy(features_.begin() + static_cast<size_t>(p) * dimension_,
-                  features_.begin() + static_cast<size_t>(p + 1) * dimension_,
-                  gather_.begin() + static_cast<size_t>(i) * dimension_);
-    }
-    ++launches_;
-    if (gmm_score_host(handle_, gather_.data(), length, dimension_, gatherScores_.data(),
-                       assigning_ ? gatherBest_.data() : nullptr, length) != GMM_OK)
-        return;
-    for (uint32_t i = 0; i < length; ++i) {
-        const uint32_t p = (featureIndex + i) % b;
-        for (uint32_t e = 0; e < nMixtures_; ++e) {
-            scores_[static_cast<size_t>(e) * b + p] = gatherScores_[static_cast<size_t>(e) * length + i];
-            if (assigning_)
-                best_[static_cast<size_t>(e) * b + p] = gatherBest_[static_cast<size_t>(e) * length + i];
-        }
-        cached_[p] = 1;
+    uint32_t p = featureIndex % b, left = length;
+    while (left > 0) {
+        const uint32_t n = std::min(left, b - p);
+        ++launches_;
+        if (gmm_score_host(handle_, features_.data() + static_cast<size_t>(p) * dimension_, n, dimension_,
+                           scores_.data() + p, assigning_ ? best_.data() + p : nullptr, b) != GMM_OK)
+            criticalError("gmm_score_host");
+        for (uint32_t i = 0; i < n; ++i)
+            cached_[p + i] = 1;
+        left -= n;
+        p = (p + n) % b;
     }
 }
 

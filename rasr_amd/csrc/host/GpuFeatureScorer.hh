@@ -9,8 +9,11 @@
 // bodies of Mm::FeatureScorer subclasses (INTEGRATION.md shows the registration).
 //
 // Errors: the constructors never throw; create() returns nullptr and sets *error (the reference
-// calls criticalError(), src/Mm/Module.cc:305).  Methods keep the reference's require()
-// preconditions as assertions.
+// calls criticalError(), src/Mm/Module.cc:305).  A failure while scoring (a device error) is never
+// answered with stale or missing scores: it goes to the critical-error handler, which aborts with
+// gmm_last_error() by default (Core::Component::criticalError); an RASR build routes it to the
+// component's own criticalError (integration/rasr/Mm/GpuFeatureScorer.cc).  Methods keep the
+// reference's require() preconditions as assertions.
 #pragma once
 
 #include <cstdint>
@@ -28,6 +31,38 @@ typedef float                    Score;            // Mm::Score (src/Mm/Types.hh
 typedef uint32_t                 EmissionIndex;    // Mm::EmissionIndex
 typedef uint32_t                 DensityInMixture; // Mm::DensityInMixture
 typedef std::vector<float>       FeatureVector;    // Mm::FeatureVector
+
+// Critical errors while scoring (Core::Component::criticalError, src/Core/Component.hh): the handler
+// must not return normally into the scorer (abort, exit or throw); the default prints the message and
+// aborts.  Returns the previous handler.
+typedef void (*CriticalErrorHandler)(const std::string& message);
+CriticalErrorHandler setCriticalErrorHandler(CriticalErrorHandler handler);
+
+// Page-locked host table (gmm_host_alloc): gmm_score_host writes it by DMA directly.
+template <class T>
+class HostTable {
+public:
+    HostTable() {}
+    HostTable(const HostTable&) = delete;
+    HostTable& operator=(const HostTable&) = delete;
+    ~HostTable() { gmm_host_free(p_); }
+    bool allocate(size_t n, T fill) {
+        gmm_host_free(p_);
+        p_ = nullptr;
+        void* q = nullptr;
+        if (gmm_host_alloc(n * sizeof(T), &q) != GMM_OK)
+            return false;
+        p_ = static_cast<T*>(q);
+        for (size_t i = 0; i < n; ++i)
+            p_[i] = fill;
+        return true;
+    }
+    T*       data() const { return p_; }
+    T&       operator[](size_t i) const { return p_[i]; }
+
+private:
+    T* p_ = nullptr;
+};
 
 // ---------------------------------------------------------------------------
 // MixtureSet: the tables of Mm::MixtureSet the scorers read (src/Mm/MixtureSet.hh:140-212)
@@ -167,13 +202,12 @@ private:
     void fill(uint32_t featureIndex, uint32_t length) const;
 
     uint32_t                      bufferSize_ = 4;
-    mutable std::vector<float>    features_;   // [bufferSize][dimension]
-    mutable std::vector<float>    scores_;     // [nMixtures][bufferSize] (BatchFeatureScorer.hh:177-186)
-    mutable std::vector<uint32_t> best_;       // [nMixtures][bufferSize]
+    mutable std::vector<float>    features_;   // [bufferSize][dimension] ring, row = buffer position
+    // [nMixtures][bufferSize] (BatchFeatureScorer.hh:177-186), page-locked: a fill writes the columns of
+    // its buffer positions straight from the device (score stride = bufferSize), no staging copy
+    HostTable<float>              scores_;
+    HostTable<uint32_t>           best_;
     mutable std::vector<char>     cached_;     // [bufferSize] (all mixtures of a position at once)
-    mutable std::vector<float>    gather_;     // staging for one launch
-    mutable std::vector<float>    gatherScores_;
-    mutable std::vector<uint32_t> gatherBest_;
     mutable int32_t               currentFeature_ = 0;
     mutable int32_t               buffered_       = 0;
     mutable uint32_t              launches_       = 0;

@@ -259,20 +259,35 @@ int nn_score_host(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_t 
         return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
     if (nFrames == 0)
         return GMM_OK;
+    const uint32_t K = s->layers[0].K, M = s->layers.back().M;
+    if (frameStride < K || scoreStride < nFrames)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frame/score stride");
     NN_HIP_CHECK(hipSetDevice(s->device));
-    const uint32_t M = s->layers.back().M;
-    float *        dF = nullptr, *dS = nullptr;
-    NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&dF), static_cast<size_t>(nFrames) * frameStride * sizeof(float)));
-    NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&dS), static_cast<size_t>(M) * scoreStride * sizeof(float)));
-    NN_HIP_CHECK(hipMemcpy(dF, frames, static_cast<size_t>(nFrames) * frameStride * sizeof(float), hipMemcpyHostToDevice));
-    int rc = nn_score_device(s, dF, nFrames, frameStride, dS, scoreStride, nullptr);
-    if (rc == GMM_OK) {
-        NN_HIP_CHECK(hipDeviceSynchronize());
-        NN_HIP_CHECK(hipMemcpy(scores, dS, static_cast<size_t>(M) * scoreStride * sizeof(float), hipMemcpyDeviceToHost));
+    // device staging: dense [nFrames][K] frames and [M][nFrames] scores; freed on every path
+    struct DeviceBuffers {
+        float* f = nullptr;
+        float* s = nullptr;
+        ~DeviceBuffers() {
+            (void)hipFree(f);
+            (void)hipFree(s);
+        }
+    } d;
+    NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d.f), static_cast<size_t>(nFrames) * K * sizeof(float)));
+    NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d.s), static_cast<size_t>(M) * nFrames * sizeof(float)));
+    // only the caller's K used floats per frame row are read, only its first nFrames columns per class row
+    // written (the rest of a strided caller buffer stays untouched, as with gmm_score_host)
+    NN_HIP_CHECK(hipMemcpy2D(d.f, static_cast<size_t>(K) * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
+                             static_cast<size_t>(K) * sizeof(float), nFrames, hipMemcpyHostToDevice));
+    const int rc = nn_score_device(s, d.f, nFrames, K, d.s, nFrames, nullptr);
+    if (rc != GMM_OK) {
+        (void)hipDeviceSynchronize();  // nothing of this call may still run when the buffers are freed
+        return rc;
     }
-    (void)hipFree(dF);
-    (void)hipFree(dS);
-    return rc;
+    NN_HIP_CHECK(hipDeviceSynchronize());
+    NN_HIP_CHECK(hipMemcpy2D(scores, static_cast<size_t>(scoreStride) * sizeof(float), d.s,
+                             static_cast<size_t>(nFrames) * sizeof(float), static_cast<size_t>(nFrames) * sizeof(float), M,
+                             hipMemcpyDeviceToHost));
+    return GMM_OK;
 }
 
 int nn_scorer_set_timing(nn_scorer* s, int enable) {

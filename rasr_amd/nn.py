@@ -143,12 +143,16 @@ class NnScorer:
                                        ctypes.c_void_p(scores.data_ptr()), int(scores.stride(0)),
                                        ctypes.c_void_p(s) if s else None), "nn_score_device")
 
-    def score_host(self, frames: np.ndarray) -> np.ndarray:
+    def score_host(self, frames: np.ndarray, out: np.ndarray | None = None, n_frames: int | None = None) -> np.ndarray:
+        """nn_score_host.  frames: [F][>= input_dim] f32 rows (row stride = frames.shape[1]); out: optional
+        caller-kept [n_classes][>= F] table (row stride = out.shape[1]), only its first F columns are written."""
         frames = np.ascontiguousarray(frames, dtype=np.float32)
-        f = frames.shape[0]
-        scores = np.empty((self.n_classes(), f), dtype=np.float32)
+        f = frames.shape[0] if n_frames is None else int(n_frames)
+        scores = np.empty((self.n_classes(), f), dtype=np.float32) if out is None else out
+        if scores.dtype != np.float32 or not scores.flags.c_contiguous or scores.ndim != 2 or scores.shape[1] < f:
+            raise ValueError("out must be a C-contiguous f32 [n_classes][>= n_frames] array")
         _check(self._l.nn_score_host(self._h, frames.ctypes.data_as(ctypes.c_void_p), f, frames.shape[1],
-                                     scores.ctypes.data_as(ctypes.c_void_p), f), "nn_score_host")
+                                     scores.ctypes.data_as(ctypes.c_void_p), scores.shape[1]), "nn_score_host")
         return scores
 
     def set_timing(self, enable: bool) -> None:

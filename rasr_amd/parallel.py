@@ -175,7 +175,7 @@ class HipShardOps:
             off = self._offsets[offset] = torch.tensor([offset], dtype=torch.int32, device=self.device)
         _capi.check(_capi.load_library().gmm_shard_pack_keys(
             scores_row.data_ptr(), None if best_row is None else best_row.data_ptr(), off.data_ptr(), 1, n,
-            scores_row.shape[-1], keys_row.data_ptr(), _stream_handle(stream)), "gmm_shard_pack_keys")
+            scores_row.shape[-1], keys_row.data_ptr(), _stream_handle(stream, self.device)), "gmm_shard_pack_keys")
 
     def unpack(self, keys, want_best: bool, stream):
         import torch
@@ -185,8 +185,14 @@ class HipShardOps:
         b_rows = torch.empty((rows, n), dtype=torch.int32, device=keys.device) if want_best else None
         _capi.check(_capi.load_library().gmm_shard_unpack_keys(
             keys.data_ptr(), rows, n, s_rows.data_ptr(), None if b_rows is None else b_rows.data_ptr(), n,
-            _stream_handle(stream)), "gmm_shard_unpack_keys")
+            _stream_handle(stream, self.device)), "gmm_shard_unpack_keys")
         return s_rows, b_rows
+
+
+# scorer types whose mixture score is the minimum over its densities' scores (so a mixture split between
+# shards is combined exactly by a per-frame minimum)
+MIN_REDUCIBLE_TYPES = frozenset({"SIMD-diagonal-maximum", "diagonal-maximum", "batch-diagonal-maximum-int",
+                                 "batch-diagonal-maximum-float", "batch-diagonal-maximum-fast"})
 
 
 class DensityShardedScorer:
@@ -197,6 +203,14 @@ class DensityShardedScorer:
     def __init__(self, mixture_set, scorer_type, max_frames: int, rank: int, world: int, device: int = 0,
                  group=None, ops=None, **kw):
         import torch
+        from . import _capi
+        name = scorer_type if isinstance(scorer_type, str) else next(
+            (k for k, v in _capi.SCORER_TYPES.items() if v == int(scorer_type)), str(scorer_type))
+        if name not in MIN_REDUCIBLE_TYPES:
+            # a split mixture's parts meet in an element-wise minimum: exact for the max-approximation scorers
+            # only (diagonal-sum needs a log-add of the partial sums; the preselection types cluster the
+            # densities of the whole set, which a shard's sub-model would not reproduce)
+            raise ValueError(f"density sharding supports {sorted(MIN_REDUCIBLE_TYPES)}, not {scorer_type!r}")
         self.ops = ops or HipShardOps(device)
         self.shards = density_shards(mixture_set.mixture_offsets, world)
         self.split = split_mixtures(self.shards)
@@ -256,9 +270,13 @@ class DensityShardedScorer:
         return full, fullb
 
 
-def _stream_handle(stream):
+def _stream_handle(stream, device=None):
+    """Raw hipStream_t for the C-ABI.  None means torch's current stream on `device` (as
+    Scorer.score_device resolves it), never the legacy null stream: the key packing must be ordered
+    after the scoring and before the RCCL collectives, which both run on the current stream."""
     if stream is None:
-        return None
+        import torch
+        stream = torch.cuda.current_stream(device)
     return ctypes_stream(stream)
 
 

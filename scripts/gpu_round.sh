@@ -20,15 +20,16 @@ STEPS=${STEPS:-"pytest smoke bench_fp32 bench_simd prof pmc"}
 for s in $STEPS; do
   case $s in
     pytest) step pytest 1200 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread ;;
-    bench) step bench 600 python bench.py ;;
+    bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_fp32) step bench_fp32 600 python bench.py --mode fp32 --steps 20 --warmup 3 ;;
     bench_simd) step bench_simd 600 python bench.py --mode simd --steps 20 --warmup 3 --cpu-baseline off ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --mode fp32 --steps 10 --warmup 2 --cpu-baseline off ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off --host-boundary off ;;
     pmc) step pmc_fp32 900 bash scripts/profile_pmc.sh fp32 &&
          step pmc_simd 900 bash scripts/profile_pmc.sh simd &&
          python scripts/pmc_summary.py $OUT/pmc_fp32 scoreSplit --json $OUT/pmc_fp32.json > /dev/null &&
          python scripts/pmc_summary.py $OUT/pmc_simd scoreI8 --json $OUT/pmc_simd.json > /dev/null ;;
+    pytest_new) step pytest_new 1200 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $PYTEST_ARGS ;;
   esac
 done
 echo done

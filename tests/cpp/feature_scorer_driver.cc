@@ -2,7 +2,12 @@
 // (src/Speech/Recognizer.cc:198-206 leaveSpeechSegment, :272-282 processFeature) and dumps every
 // ContextScorer's scores, so tests/test_host_protocol.py can compare them with the oracle.
 //
-// usage: feature_scorer_driver <model> <frames.bin> <out.bin> <type> <bufferSize> <segments>
+// usage: feature_scorer_driver <model> <frames.bin> <out.bin> <type> <bufferSize> <segments> [protocol]
+//   protocol  : "recognizer" (default): Speech::OfflineRecognizer, reset() before every segment,
+//               scores as the search reads them;
+//               "node": Speech::FeatureScorerNode::work (src/Speech/FeatureScorerNode.cc:113-162), the
+//               reference's score dump: every frame's -score(e) for ALL emissions (putData, :95-111),
+//               finalize() and reset() after every segment
 //   model     : a RASR mixture-set text file (*.pms, *.pms.gz; MixtureSet::read) or
 //   model.bin : u32 D, nMeans, nCov, nDens, nMix, nEntries; f32 means[nMeans*D]; f32 var[nCov*D];
 //               u32 densMean[nDens]; u32 densCov[nDens]; u32 offsets[nMix+1]; u32 dens[nEntries];
@@ -53,10 +58,14 @@ static std::unique_ptr<Mm::Gpu::MixtureSet> readBinaryModel(const std::string& p
 }
 
 int main(int argc, char** argv) {
-    if (argc != 7) {
-        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments\n", argv[0]);
+    if (argc != 7 && argc != 8) {
+        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node]\n", argv[0]);
         return 2;
     }
+    const std::string protocol = argc == 8 ? argv[7] : "recognizer";
+    if (protocol != "recognizer" && protocol != "node")
+        return 2;
+    const bool node = protocol == "node";
     const std::string modelPath(argv[1]);
     const bool        pms = modelPath.size() > 4 && (modelPath.find(".pms") != std::string::npos);
     FILE*             ff  = fopen(argv[2], "rb");
@@ -99,25 +108,31 @@ int main(int argc, char** argv) {
     std::vector<float>    outS;
     std::vector<uint32_t> outB;
     auto consume = [&](const Mm::Gpu::Scorer& s) {  // the search reads score(e) for active e
-        for (uint32_t e = 0; e < M; ++e) {
-            outS.push_back(s->score(e));
+        const uint32_t n = node ? s->nEmissions() : M;  // the node dumps nEmissions() values per frame
+        for (uint32_t e = 0; e < n; ++e) {
+            outS.push_back(node ? -s->score(e) : s->score(e));  // FeatureScorerNode::putData: +log space
             outB.push_back(s->hasBestDensity() ? s->bestDensity(e) : 0xffffffffu);
         }
     };
     const uint32_t segments = static_cast<uint32_t>(atoi(argv[6]));
     for (uint32_t seg = 0; seg < segments; ++seg) {
-        scorer->reset();
+        if (!node)
+            scorer->reset();  // Recognizer.cc:186
         const uint32_t t0 = F * seg / segments, t1 = F * (seg + 1) / segments;
         for (uint32_t t = t0; t < t1; ++t) {
             Mm::Gpu::FeatureVector f(frames.begin() + size_t(t) * D, frames.begin() + size_t(t + 1) * D);
-            if (scorer->isBuffered() && !scorer->bufferFilled())  // Recognizer.cc:275-277
+            if (scorer->isBuffered() && !scorer->bufferFilled())  // Recognizer.cc:275-277, FeatureScorerNode.cc:131-134
                 scorer->addFeature(f);
             else
                 consume(scorer->getScorer(f));
         }
-        if (scorer->isBuffered())  // Recognizer.cc:200-204
+        if (scorer->isBuffered())  // Recognizer.cc:200-204, FeatureScorerNode.cc:148-154
             while (!scorer->bufferEmpty())
                 consume(scorer->flush());
+        if (node) {  // FeatureScorerNode.cc:157-159
+            scorer->finalize();
+            scorer->reset();
+        }
     }
     uint32_t launches = 0;
     if (auto* b = dynamic_cast<Mm::Gpu::GpuBatchFeatureScorer*>(scorer.get()))

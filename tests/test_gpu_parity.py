@@ -182,6 +182,55 @@ def test_float_extreme_frames(gpu, kopts):
     _check_float(s, b, ref_s, ref_b, ms, frames, None)
 
 
+def _offset_model(m, k, d, c=1, seed=41):
+    """Offset, narrow Gaussians: mu ~ N(20, 1) in every other dimension (N(0, 1) in the rest), variances
+    U[0.01, 0.1]: |mu / sigma| up to ~200, the regime where the expanded form ||x'||^2 + ||m'||^2 - 2 x'.m'
+    of the float kernels cancels (the reference takes (mu - x) isv before squaring,
+    GaussDiagonalMaximumFeatureScorer.cc:144-218)."""
+    base = _model(m, k, d, c, "random", seed=seed)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    means = base.means.copy()
+    means[:, ::2] += np.float32(20.0)
+    var = rng.uniform(0.01, 0.1, (c, d)).astype(np.float32)
+    return ra.MixtureSet(means, var, base.density_mean, base.density_covariance, base.mixture_offsets,
+                         base.mixture_densities, base.mixture_log_weights)
+
+
+def _frames_near(ms, n, seed, spread=0.05):
+    """Frames at mu_d +- spread * sigma of randomly chosen densities d (the score is then dominated by the
+    row constant and a small distance), plus every 8th frame drawn around the model centre."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    dens = rng.integers(0, ms.n_densities, n)
+    sd = np.sqrt(ms.variances[ms.density_covariance[dens]])
+    frames = ms.means[ms.density_mean[dens]] + spread * sd * rng.choice([-1.0, 1.0], size=(n, ms.dimension))
+    frames[::8] = ms.means.mean(0) + rng.standard_normal((len(frames[::8]), ms.dimension))
+    return frames.astype(np.float32)
+
+
+@pytest.mark.parametrize("kopts", FLOAT_KERNELS)
+@pytest.mark.parametrize("dim", [39, 45])
+def test_float_offset_narrow_gaussians(gpu, kopts, dim):
+    """Float contract (1e-4 relative) on models far from the origin with narrow variances and frames close
+    to a density: the case where an expanded quadratic form about the origin loses ~1e-3."""
+    ms = _offset_model(80, "ragged", dim)
+    frames = _frames_near(ms, 400, seed=43)
+    ref_s, ref_b = oracle.OracleFloat(ms).score(frames, n_threads=8)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum", **kopts)
+    _check_float(s, b, ref_s, ref_b, ms, frames, None)
+    ref = oracle.batch_float_score(ms, frames, n_threads=8)
+    s2, _ = _gpu_scores(ms, frames, "batch-diagonal-maximum-float", **kopts)
+    _assert_close(s2, ref)
+
+
+def test_float_offset_narrow_gaussians_multi_covariance(gpu):
+    """Several covariances (scoreF32 with ||x'||^2 folded into K) on the offset, narrow model."""
+    ms = _offset_model(40, 12, 39, c=3)
+    frames = _frames_near(ms, 300, seed=44)
+    ref_s, ref_b = oracle.OracleFloat(ms).score(frames, n_threads=8)
+    s, b = _gpu_scores(ms, frames, "diagonal-maximum")
+    _check_float(s, b, ref_s, ref_b, ms, frames, None)
+
+
 def _edge_model():
     """Mixtures with 0, 1, 16, 17 densities, duplicated densities (exact ties), shared densities."""
     rng = np.random.Generator(np.random.PCG64(5))
@@ -268,13 +317,15 @@ def test_quantization_accessors(gpu):
     assert np.array_equal(sc.multiply_and_quantize(x), o.quantize_frame(x))
 
 
+@pytest.mark.parametrize("dim", [39, 45])
 @pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum", "diagonal-maximum/split32",
-                                  "diagonal-maximum/native"])
-def test_full_size_800k_subset(gpu, kind):
-    """BASELINE config 2 model (5000 x 160 densities, D=39): GPU vs oracle on 96 frames."""
+                                  "diagonal-maximum/split16", "diagonal-maximum/native"])
+def test_full_size_800k_subset(gpu, kind, dim):
+    """BASELINE config 2 (5000 x 160 densities, D=39) and config 3 (the same at D=45, LDA+MLLT
+    features; default float kernel scoreSplit32) models: GPU vs oracle on 96 frames."""
     import torch
-    ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
-    frames = ra.synthetic_frames(96, 39, seed=77)
+    ms = ra.synthetic_mixture_set(5000, 160, dim, seed=2024)
+    frames = ra.synthetic_frames(96, dim, seed=77)
     kind, _, opt = kind.partition("/")
     if kind == "SIMD-diagonal-maximum":
         ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames, n_threads=16)
@@ -314,3 +365,23 @@ def test_full_size_batch_invariance(gpu, kind):
     assert torch.equal(fullb, partb)
     assert torch.isfinite(full).all()
     assert int(fullb.min()) >= 0 and int(fullb.max()) < 160
+
+
+@pytest.mark.parametrize("dim", [39, 45, 33, 48])
+def test_batch_fast_bit_exact(gpu, dim):
+    """batch-diagonal-maximum-fast (BatchUnrolledIntFeatureScorer, BatchFeatureScorer.cc:558-604) against its
+    restatement with the fixed 48-byte loads and mean stride: bit-exact at padded dimension 48."""
+    ms = _model(45, "ragged", dim, 1, "random", seed=dim)
+    frames = ra.synthetic_frames(300, dim, seed=dim + 1)
+    ref = oracle.batch_fast_score(ms, frames)
+    s, _ = _gpu_scores(ms, frames, "batch-diagonal-maximum-fast")
+    _assert_bit_exact(s, ref)
+
+
+@pytest.mark.parametrize("dim", [16, 20, 32, 49])
+def test_batch_fast_refuses_other_dimensions(gpu, dim):
+    """Padded dimension 16 / 32: the reference's unrolled loop reads other rows and past its allocation
+    (undefined); > 48: refused by the reference itself (cc:552-555)."""
+    ms = _model(5, 4, dim, 1, "random")
+    with pytest.raises(ra.GmmError):
+        ra.Scorer(ms, "batch-diagonal-maximum-fast", max_frames=8)

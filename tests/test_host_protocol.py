@@ -27,7 +27,7 @@ def _write_model(path, ms):
         ms.mixture_log_weights.astype(np.float64).tofile(f)
 
 
-def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None):
+def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, protocol="recognizer"):
     mp, fp, op = tmp_path / "m.bin", tmp_path / "f.bin", tmp_path / "o.bin"
     if model_file is None:
         _write_model(mp, ms)
@@ -36,7 +36,7 @@ def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None):
     with open(fp, "wb") as f:
         np.array(frames.shape, dtype=np.uint32).tofile(f)
         frames.astype(np.float32).tofile(f)
-    subprocess.run([DRIVER, str(mp), str(fp), str(op), kind, str(buffer_size), str(segments)], check=True,
+    subprocess.run([DRIVER, str(mp), str(fp), str(op), kind, str(buffer_size), str(segments), protocol], check=True,
                    timeout=300)
     raw = np.fromfile(op, dtype=np.uint32)
     F, M, launches = raw[:3]
@@ -123,3 +123,24 @@ def test_preselection_protocol(gpu, tmp_path, kind):
     else:
         err = np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))
         assert err.max() <= 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,buffer_size", [("SIMD-diagonal-maximum", 1), ("SIMD-diagonal-maximum", 6),
+                                              ("batch-diagonal-maximum-int", 4), ("diagonal-maximum", 5)])
+def test_feature_scorer_node_dump(gpu, tmp_path, kind, buffer_size):
+    """Speech::FeatureScorerNode (src/Speech/FeatureScorerNode.cc:95-162), the reference's score dump: every
+    frame yields -score(e) for all nEmissions() mixtures, in frame order, with finalize() + reset() after each
+    segment.  Compared with the oracle's scores negated."""
+    ms = ra.synthetic_mixture_set(28, 10, 39, seed=49, weights="random")
+    frames = ra.synthetic_frames(47, 39, seed=50)
+    s, b, _ = _run(tmp_path, ms, frames, kind, buffer_size, 3, protocol="node")
+    if kind == "SIMD-diagonal-maximum":
+        ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+        assert np.array_equal(s.T.view(np.uint32), (-ref_s).view(np.uint32))
+        assert np.array_equal(b.T, ref_b)
+    elif kind == "batch-diagonal-maximum-int":
+        assert np.array_equal(s.T.view(np.uint32), (-oracle.batch_int_score(ms, frames)).view(np.uint32))
+    else:
+        ref = -oracle.OracleFloat(ms).score(frames)[0]
+        assert (np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))).max() <= 1e-4

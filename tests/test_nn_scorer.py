@@ -74,6 +74,14 @@ def test_nn_scorer_device_strides_and_errors(gpu):
     o = out.cpu().numpy()
     assert _err(o[:, :130], ref) <= 2e-3
     assert (o[:, 130:] == 7.0).all()  # nothing written past n_frames
+    # host path with strided caller buffers: frame rows of 48 floats (39 used, the rest a sentinel that must
+    # not be read as features), a score table of 160 columns of which only the first 130 are written
+    xs = np.full((130, 48), np.nan, np.float32)
+    xs[:, :39] = x
+    table = np.full((200, 160), 7.0, np.float32)
+    sc.score_host(xs, out=table)
+    assert _err(table[:, :130], ref) <= 2e-3
+    assert (table[:, 130:] == 7.0).all()
     with pytest.raises(ra.GmmError):
         sc.score_host(ra.synthetic_frames(131, 39, seed=1))  # more than max_frames
     with pytest.raises(ra.GmmError):
