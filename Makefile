@@ -21,7 +21,7 @@ HDRS      = include/rasr_gmm.h $(SRC)/gmm_presel.hh $(SRC)/gmm_prepare.hh $(SRC)
 
 LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
-            $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
+            $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/MixtureSetEstimatorFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
             $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o $(BUILD)/gmm_kernels_shard.o $(BUILD)/gmm_hostio.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
@@ -81,6 +81,10 @@ $(BUILD)/GpuFeatureScorer.o: $(SRC)/host/GpuFeatureScorer.cc $(HDRS)
 	g++ $(HOSTFLAGS) -c $< -o $@
 
 $(BUILD)/MixtureSetFile.o: $(SRC)/host/MixtureSetFile.cc $(HDRS)
+	@mkdir -p $(BUILD)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
+$(BUILD)/MixtureSetEstimatorFile.o: $(SRC)/host/MixtureSetEstimatorFile.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	g++ $(HOSTFLAGS) -c $< -o $@
 

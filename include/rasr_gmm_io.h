@@ -7,6 +7,7 @@
  * chain for this format:
  *   Mm::Module_::readMixtureSet        src/Mm/Module.cc:152-182
  *   MixtureSetReader::FormatReader     src/Mm/MixtureSetReader.cc:28-47
+ *   MixtureSetEstimatorReader          src/Mm/MixtureSetReader.cc:52-74 (binary estimator files, below)
  *   Core::CompressedPlainTextFormat    src/Core/FormatSet.hh:302-320 (gzip detected from the data)
  *   MixtureSet::read / ::write         src/Mm/MixtureSet.cc:142-214
  *   Mixture::read / ::write            src/Mm/Mixture.cc:81-107
@@ -37,8 +38,41 @@
 extern "C" {
 #endif
 
+/* Parameters of the maximum-likelihood estimation that turns an estimator (accumulator) file into a
+ * mixture set (AbstractMixtureSetEstimator, src/Mm/AbstractMixtureSetEstimator.cc:25-58; the reader takes
+ * them from the mixture-set configuration). */
+typedef struct {
+    double   minimum_observation_weight; /* "minimum-observation-weight" (5): densities of a mixture with less
+                                            accumulated weight are removed (except the heaviest one)        */
+    double   minimum_relative_weight;    /* "minimum-relative-weight" (0), relative to the mixture's weight   */
+    double   minimum_variance;           /* "minimum-variance" (0): variances below are raised to it          */
+    uint32_t allow_zero_weights;         /* "allow-zero-weights" (false): else a zero-weight mixture fails    */
+    uint32_t normalize_mixture_weights;  /* "normalize-mixture-weights" (true)                               */
+} gmm_estimator_config;
+
+void gmm_default_estimator_config(gmm_estimator_config* config);
+
+/* Estimate a mixture set from the bytes of a binary maximum-likelihood estimator file ("MIXSET" magic,
+ * written by RASR's trainers, AbstractMixtureSetEstimator::write, cc:481-509): the reference's
+ * MixtureSetReader::MixtureSetEstimatorReader (src/Mm/MixtureSetReader.cc:52-74) = estimator->read
+ * (AbstractMixtureSetEstimator.cc:433-479) then estimate() (:299-337): densities below the minimum weights
+ * removed, means = sums / weight, pooled variances = (sum of squares - sum over the covariance's means of
+ * mean sum^2 / mean weight) / weight, raised to minimum_variance, mixture log weights normalized.  Errors:
+ * GMM_ERR_INVALID_ARGUMENT for a wrong magic, a truncated file, out-of-range indices, accumulators whose size
+ * differs from the dimension, a zero-weight mixture (unless allowed) or a mixture without densities,
+ * a covariance whose weight differs from its means' (the reference's criticalError / verify). */
+int gmm_mixture_set_estimate(const void* data, uint64_t size, const gmm_estimator_config* config,
+                             gmm_mixture_set* out);
+
+/* gmm_mixture_set_read with explicit estimator parameters (NULL = defaults). */
+int gmm_mixture_set_read_config(const char* filename, const gmm_estimator_config* config, uint32_t dimension_offset,
+                                uint32_t reduced_dimension, gmm_mixture_set* out);
+
 /* Read a mixture-set file into *out (arrays allocated by the library; release
- * them with gmm_mixture_set_free).  dimension_offset / reduced_dimension are the
+ * them with gmm_mixture_set_free).  The format follows the reference's reader dispatch on the file name
+ * extension (MixtureSetReader.cc:28-35, MixtureSetReader.hh:105-117, Core::filenameExtension): ".pms" and
+ * ".gz" are the text format below, every other name a binary estimator file (gmm_mixture_set_estimate with
+ * the default parameters).  dimension_offset / reduced_dimension are the
  * "reduced-mixture-set-dimension-offset" / "reduced-mixture-set-dimension"
  * parameters (Module.cc:42-49, applied at :165-175): the first
  * dimension_offset components of every mean and covariance are dropped, then,

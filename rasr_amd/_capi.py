@@ -77,6 +77,16 @@ class ScorerConfig(ctypes.Structure):
     ]
 
 
+class EstimatorConfig(ctypes.Structure):
+    _fields_ = [
+        ("minimum_observation_weight", ctypes.c_double),
+        ("minimum_relative_weight", ctypes.c_double),
+        ("minimum_variance", ctypes.c_double),
+        ("allow_zero_weights", ctypes.c_uint32),
+        ("normalize_mixture_weights", ctypes.c_uint32),
+    ]
+
+
 # (name, restype, argtypes) for every function declared in include/rasr_gmm.h and rasr_gmm_io.h
 PROTOTYPES = [
     ("gmm_default_config", None, [ctypes.POINTER(ScorerConfig)]),
@@ -123,6 +133,12 @@ PROTOTYPES = [
     ("gmm_mixture_set_parse", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(MixtureSetDesc)]),
     ("gmm_mixture_set_free", ctypes.c_int, [ctypes.POINTER(MixtureSetDesc)]),
+    ("gmm_default_estimator_config", None, [ctypes.POINTER(EstimatorConfig)]),
+    ("gmm_mixture_set_estimate", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(EstimatorConfig), ctypes.POINTER(MixtureSetDesc)]),
+    ("gmm_mixture_set_read_config", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.POINTER(EstimatorConfig), ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.POINTER(MixtureSetDesc)]),
     ("gmm_mixture_set_write", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MixtureSetDesc), ctypes.c_uint32]),
     ("gmm_version", ctypes.c_char_p, []),
 ]

@@ -84,8 +84,9 @@ public:
     // descriptor of the C-ABI (valid while this object is alive and unchanged)
     gmm_mixture_set descriptor() const;
 
-    // Module_::readMixtureSet (src/Mm/Module.cc:152-182) for the text format (".pms", ".pms.gz"),
-    // via gmm_mixture_set_read (include/rasr_gmm_io.h); nullptr and *error on failure
+    // Module_::readMixtureSet (src/Mm/Module.cc:152-182) via gmm_mixture_set_read (include/rasr_gmm_io.h):
+    // the text format for ".pms" / ".gz" names, a binary maximum-likelihood estimator file (estimated with the
+    // default parameters) for any other name; nullptr and *error on failure
     static std::unique_ptr<MixtureSet> read(const std::string& filename, std::string* error,
                                             uint32_t dimensionOffset = 0, uint32_t reducedDimension = 0);
 

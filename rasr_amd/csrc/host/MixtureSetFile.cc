@@ -380,6 +380,45 @@ bool reshapeRows(const std::vector<float>& data, const std::vector<uint64_t>& of
 }
 
 template <class T>
+T* copyOut(const std::vector<T>& v);
+
+// Module_::readMixtureSet's offset / reduced dimension (Module.cc:165-175) on a set already in tables
+int offsetAndReduce(gmm_mixture_set* ms, uint32_t offset, uint32_t reduced) {
+    if (offset == 0 && reduced == 0)
+        return GMM_OK;
+    Status                st;
+    const uint32_t        D = ms->dimension, dim = reduced > 0 ? reduced : (offset <= D ? D - offset : 0);
+    std::vector<float>    m(ms->means, ms->means + size_t(ms->n_means) * D), v(ms->variances, ms->variances + size_t(ms->n_covariances) * D);
+    std::vector<uint64_t> mo(ms->n_means + 1), vo(ms->n_covariances + 1);
+    for (size_t i = 0; i < mo.size(); ++i)
+        mo[i] = i * D;
+    for (size_t i = 0; i < vo.size(); ++i)
+        vo[i] = i * D;
+    std::vector<float> means, vars;
+    if (!reshapeRows(m, mo, offset, reduced, dim, 0.0f, "mean", means, st) ||
+        !reshapeRows(v, vo, offset, reduced, dim, 1.0f, "covariance", vars, st)) {
+        gmm_mixture_set_free(ms);
+        setLastError(st.msg);
+        return st.code;
+    }
+    float* nm = copyOut(means);
+    float* nv = copyOut(vars);
+    if (!nm || !nv) {
+        std::free(nm);
+        std::free(nv);
+        gmm_mixture_set_free(ms);
+        setLastError("mixture set: out of host memory");
+        return GMM_ERR_OUT_OF_MEMORY;
+    }
+    std::free(const_cast<float*>(ms->means));
+    std::free(const_cast<float*>(ms->variances));
+    ms->means     = nm;
+    ms->variances = nv;
+    ms->dimension = dim;
+    return GMM_OK;
+}
+
+template <class T>
 T* copyOut(const std::vector<T>& v) {
     T* p = static_cast<T*>(std::malloc(std::max<size_t>(v.size(), 1) * sizeof(T)));
     if (p && !v.empty())
@@ -544,6 +583,11 @@ int gmm_mixture_set_parse(const void* data, uint64_t size, uint32_t dimension_of
 
 int gmm_mixture_set_read(const char* filename, uint32_t dimension_offset, uint32_t reduced_dimension,
                          gmm_mixture_set* out) {
+    return gmm_mixture_set_read_config(filename, nullptr, dimension_offset, reduced_dimension, out);
+}
+
+int gmm_mixture_set_read_config(const char* filename, const gmm_estimator_config* config, uint32_t dimension_offset,
+                                uint32_t reduced_dimension, gmm_mixture_set* out) {
     if (!filename || !out) {
         setLastError("gmm_mixture_set_read: null argument");
         return GMM_ERR_INVALID_ARGUMENT;
@@ -565,8 +609,16 @@ int gmm_mixture_set_read(const char* filename, uint32_t dimension_offset, uint32
         setLastError(std::string("mixture set: read error on \"") + filename + "\"");
         return GMM_ERR_INVALID_ARGUMENT;
     }
-    const int rc = parseBytes(bytes.empty() ? chunk : bytes.data(), bytes.size(), dimension_offset,
-                              reduced_dimension, out);
+    // MixtureSetReader: ".pms" / ".gz" (Core::filenameExtension, the text after the last '.' of the last path
+    // component) through the format reader, any other name through the estimator reader
+    const std::string name(filename);
+    const size_t      dot = name.find_last_of("./");
+    const std::string ext = dot != std::string::npos && name[dot] == '.' ? name.substr(dot) : std::string();
+    int               rc;
+    if (ext == ".pms" || ext == ".gz")
+        rc = parseBytes(bytes.empty() ? chunk : bytes.data(), bytes.size(), dimension_offset, reduced_dimension, out);
+    else if ((rc = gmm_mixture_set_estimate(bytes.data(), bytes.size(), config, out)) == GMM_OK)
+        rc = offsetAndReduce(out, dimension_offset, reduced_dimension);
     if (rc != GMM_OK) {
         const std::string msg = std::string("\"") + filename + "\": ";
         setLastError(msg + gmm_last_error());

@@ -103,14 +103,28 @@ def _from_desc(d: _capi.MixtureSetDesc) -> MixtureSet:
         mixture_log_weights=arr(d.mixture_log_weights, n_entries, np.float64))
 
 
-def read_mixture_set(path: str, dimension_offset: int = 0, reduced_dimension: int = 0) -> MixtureSet:
-    """Read a RASR ".pms" / ".pms.gz" text mixture set through the C-ABI
-    (gmm_mixture_set_read, include/rasr_gmm_io.h; Mm::Module_::readMixtureSet,
-    src/Mm/Module.cc:152-182, with the reduced-mixture-set-dimension[-offset] parameters)."""
+def estimator_config(**kw) -> _capi.EstimatorConfig:
+    """gmm_estimator_config with the reference defaults, overridden by keyword (minimum_observation_weight,
+    minimum_relative_weight, minimum_variance, allow_zero_weights, normalize_mixture_weights)."""
+    cfg = _capi.EstimatorConfig()
+    _capi.load_library().gmm_default_estimator_config(ctypes.byref(cfg))
+    for k, v in kw.items():
+        if not hasattr(cfg, k):
+            raise TypeError(f"unknown estimator parameter {k}")
+        setattr(cfg, k, v)
+    return cfg
+
+
+def read_mixture_set(path: str, dimension_offset: int = 0, reduced_dimension: int = 0, **estimator) -> MixtureSet:
+    """Read a RASR mixture set through the C-ABI (gmm_mixture_set_read_config, include/rasr_gmm_io.h;
+    Mm::Module_::readMixtureSet, src/Mm/Module.cc:152-182, with the reduced-mixture-set-dimension[-offset]
+    parameters): ".pms" / ".gz" names as text, any other name as a binary maximum-likelihood estimator file,
+    estimated with the given parameters (estimator_config)."""
     lib = _capi.load_library()
     d = _capi.MixtureSetDesc()
-    _capi.check(lib.gmm_mixture_set_read(os.fsencode(path), dimension_offset, reduced_dimension, ctypes.byref(d)),
-                "gmm_mixture_set_read")
+    cfg = estimator_config(**estimator)
+    _capi.check(lib.gmm_mixture_set_read_config(os.fsencode(path), ctypes.byref(cfg), dimension_offset,
+                                                reduced_dimension, ctypes.byref(d)), "gmm_mixture_set_read")
     try:
         return _from_desc(d)
     finally:
@@ -124,6 +138,20 @@ def parse_mixture_set(data: bytes, dimension_offset: int = 0, reduced_dimension:
     buf = ctypes.create_string_buffer(data, len(data))
     _capi.check(lib.gmm_mixture_set_parse(buf, len(data), dimension_offset, reduced_dimension, ctypes.byref(d)),
                 "gmm_mixture_set_parse")
+    try:
+        return _from_desc(d)
+    finally:
+        lib.gmm_mixture_set_free(ctypes.byref(d))
+
+
+def estimate_mixture_set(data: bytes, **estimator) -> MixtureSet:
+    """gmm_mixture_set_estimate: the mixture set a binary estimator file's bytes describe."""
+    lib = _capi.load_library()
+    d = _capi.MixtureSetDesc()
+    cfg = estimator_config(**estimator)
+    buf = ctypes.create_string_buffer(data, len(data))
+    _capi.check(lib.gmm_mixture_set_estimate(buf, len(data), ctypes.byref(cfg), ctypes.byref(d)),
+                "gmm_mixture_set_estimate")
     try:
         return _from_desc(d)
     finally:

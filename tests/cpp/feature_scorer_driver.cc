@@ -8,8 +8,9 @@
 //               "node": Speech::FeatureScorerNode::work (src/Speech/FeatureScorerNode.cc:113-162), the
 //               reference's score dump: every frame's -score(e) for ALL emissions (putData, :95-111),
 //               finalize() and reset() after every segment
-//   model     : a RASR mixture-set text file (*.pms, *.pms.gz; MixtureSet::read) or
-//   model.bin : u32 D, nMeans, nCov, nDens, nMix, nEntries; f32 means[nMeans*D]; f32 var[nCov*D];
+//   model     : a RASR mixture-set file read by Mm::Gpu::MixtureSet::read like the reference's MixtureSetReader:
+//               text for *.pms / *.gz, a binary maximum-likelihood estimator file for any other name; or
+//   model.drvmodel : (this test's own dump) u32 D, nMeans, nCov, nDens, nMix, nEntries; f32 means[nMeans*D]; f32 var[nCov*D];
 //               u32 densMean[nDens]; u32 densCov[nDens]; u32 offsets[nMix+1]; u32 dens[nEntries];
 //               f64 logw[nEntries]
 //   frames.bin: u32 F, D; f32 frames[F*D]
@@ -67,7 +68,9 @@ int main(int argc, char** argv) {
         return 2;
     const bool node = protocol == "node";
     const std::string modelPath(argv[1]);
-    const bool        pms = modelPath.size() > 4 && (modelPath.find(".pms") != std::string::npos);
+    const std::string dump(".drvmodel");
+    const bool        pms = !(modelPath.size() >= dump.size() &&
+                              modelPath.compare(modelPath.size() - dump.size(), dump.size(), dump) == 0);
     FILE*             ff  = fopen(argv[2], "rb");
     if (!ff)
         return 2;

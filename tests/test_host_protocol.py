@@ -28,7 +28,7 @@ def _write_model(path, ms):
 
 
 def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, protocol="recognizer"):
-    mp, fp, op = tmp_path / "m.bin", tmp_path / "f.bin", tmp_path / "o.bin"
+    mp, fp, op = tmp_path / "m.drvmodel", tmp_path / "f.bin", tmp_path / "o.bin"
     if model_file is None:
         _write_model(mp, ms)
     else:
@@ -144,3 +144,23 @@ def test_feature_scorer_node_dump(gpu, tmp_path, kind, buffer_size):
     else:
         ref = -oracle.OracleFloat(ms).score(frames)[0]
         assert (np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))).max() <= 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum"])
+def test_protocol_model_from_estimator_file(gpu, tmp_path, kind):
+    """A model a trainer wrote as a binary estimator file (the reference's default reader, MixtureSetReader.cc:52-74)
+    loads through the C++ host side (Mm::Gpu::MixtureSet::read) and scores through the recognizer protocol."""
+    from oracle import estimator as est
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "estimator", "model.mix")
+    ms = ra.read_mixture_set(path)  # the estimated model
+    frames = ra.synthetic_frames(41, ms.dimension, seed=51) * 2
+    s, b, _ = _run(tmp_path, ms, frames, kind, 6, 2, model_file=path)
+    if kind == "SIMD-diagonal-maximum":
+        ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+        assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
+        assert np.array_equal(b.T, ref_b)
+    else:
+        ref = oracle.OracleFloat(ms).score(frames)[0]
+        assert (np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))).max() <= 1e-4
+    del est
