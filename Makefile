@@ -64,9 +64,17 @@ $(BUILD)/nn_api.o: $(SRC)/nn_api.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
-$(BUILD)/gmm_api.o: $(SRC)/gmm_api.cc $(HDRS)
+# identity of the device code (hash of the kernel sources and their flags): profiling summaries record it and
+# bench.py uses a summary only for the kernels it was measured on
+KERNEL_SRCS = $(SRC)/gmm_kernels_i8.hip $(SRC)/gmm_kernels_f32.hip $(SRC)/gmm_kernels_split.hip $(SRC)/gmm_kernels_presel.hip \
+              $(SRC)/gmm_kernels_shard.hip $(SRC)/nn_kernels.hip $(SRC)/gmm_device.hh $(SRC)/gmm_kernels.hh $(SRC)/nn_kernels.hh
+$(BUILD)/kernel_id.h: $(KERNEL_SRCS) Makefile
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
+	@echo "#define GMM_KERNEL_ID \"$$( (cat $(KERNEL_SRCS); echo '$(HIPFLAGS) $(I8FLAGS) $(F32FLAGS) $(SPLITFLAGS)') | sha256sum | cut -c1-16)\"" > $@
+
+$(BUILD)/gmm_api.o: $(SRC)/gmm_api.cc $(HDRS) $(BUILD)/kernel_id.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HOSTFLAGS) -I$(BUILD) -c $< -o $@
 
 $(BUILD)/gmm_hostio.o: $(SRC)/gmm_hostio.cc $(HDRS)
 	@mkdir -p $(BUILD)

@@ -40,7 +40,6 @@ page-locked table, PCIe included; never `value`).
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import math
 import os
@@ -164,26 +163,23 @@ def max_over_ranks(x: float, ws: int) -> float:
     return float(t.item())
 
 
-def _library_sha() -> str:
+def _kernel_id() -> str:
     from rasr_amd import _capi
-    h = hashlib.sha256()
-    with open(_capi.LIB_PATH, "rb") as f:
-        h.update(f.read())
-    return h.hexdigest()[:16]
+    return _capi.load_library().gmm_kernel_id().decode()
 
 
 def load_pmc(mode: str, frames_per_launch: int):
     """HBM bytes per launch of the dominant kernel from the rocprofv3 PMC summary under profiles/
     (scripts/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE), used only when it
-    was collected on this very library build and launch size; else null."""
+    was collected on this build's kernels (gmm_kernel_id) at this launch size; else null."""
     path = os.path.join(ROOT, "profiles", f"pmc_{mode}.json")
     try:
         with open(path) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
         return None, None
-    if pmc.get("library_sha") != _library_sha() or pmc.get("frames_per_launch") != frames_per_launch:
-        return None, f"{os.path.relpath(path, ROOT)} is from another build or launch size"
+    if pmc.get("kernel_id") != _kernel_id() or pmc.get("frames_per_launch") != frames_per_launch:
+        return None, f"{os.path.relpath(path, ROOT)} is from other kernels or another launch size"
     return pmc.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
@@ -440,9 +436,11 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
-    if os.environ.get("RASR_BENCH_LAUNCH_PROBE") == "1":  # tests/test_bench_launcher.py: the ranks, no GPU work
-        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world_size": int(os.environ.get("WORLD_SIZE", "1")),
-                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "gpus": args.gpus}), flush=True)
+    if os.environ.get("RASR_BENCH_LAUNCH_PROBE"):  # tests/test_bench_launcher.py: the ranks, no GPU work
+        rec = {"rank": int(os.environ.get("RANK", "0")), "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+               "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "gpus": args.gpus}
+        with open(os.path.join(os.environ["RASR_BENCH_LAUNCH_PROBE"], f"rank{rec['rank']}.json"), "w") as f:
+            json.dump(rec, f)
         return
     import rasr_amd as ra
     ws, rank, local = dist_setup(args)

@@ -196,6 +196,9 @@ int gmm_shard_unpack_keys(const int64_t* keys, uint32_t rows, uint32_t n_frames,
 
 const char* gmm_last_error(void);
 const char* gmm_version(void);
+/* Identity of this build's device code (a hash of the kernel sources and compile flags); profiling
+ * summaries record it, so a counter measurement is matched to the kernels it was taken on. */
+const char* gmm_kernel_id(void);
 
 #ifdef __cplusplus
 }

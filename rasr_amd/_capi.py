@@ -141,6 +141,7 @@ PROTOTYPES = [
       ctypes.POINTER(MixtureSetDesc)]),
     ("gmm_mixture_set_write", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MixtureSetDesc), ctypes.c_uint32]),
     ("gmm_version", ctypes.c_char_p, []),
+    ("gmm_kernel_id", ctypes.c_char_p, []),
 ]
 
 _lib = None

@@ -22,6 +22,7 @@
 #include "gmm_kernels.hh"
 #include "gmm_prepare.hh"
 #include "gmm_presel.hh"
+#include "kernel_id.h"  // build/kernel_id.h (Makefile): GMM_KERNEL_ID
 
 using namespace rasr_gmm;
 
@@ -1004,7 +1005,11 @@ const char* gmm_last_error(void) {
 }
 
 const char* gmm_version(void) {
-    return "rasr_amd-gmm 0.1 (gfx950)";
+    return "rasr_amd-gmm 0.2 (gfx950)";
+}
+
+const char* gmm_kernel_id(void) {
+    return GMM_KERNEL_ID;
 }
 
 }  // extern "C"

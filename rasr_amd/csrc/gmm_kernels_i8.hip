@@ -28,6 +28,10 @@
 // This file: the quantized kernels (built with -mllvm -amdgpu-mfma-vgpr-form, see Makefile).
 #include "gmm_device.hh"
 
+#ifndef GMM_I8_DIAG
+#define GMM_I8_DIAG 0  // timing diagnostics only (wrong results): 2 = keys without the pack, 4 = emit only the
+                       // chunk's last mixture, 8 = f32 finalize instead of the f64 division
+#endif
 #ifndef GMM_I8_INTERLEAVE
 #define GMM_I8_INTERLEAVE 4  // VALU per MFMA in a sched_group_barrier interleave of the pair step (0 = off; 4: +2 %, 6: -4 %)
 #endif
@@ -133,7 +137,9 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
             dns = static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
         }
         float score;
-        if (a.flavor == 0)  // SimdFeatureScorer.cc:142: 0.5 * q / scalingSquared_ in double
+        if (GMM_I8_DIAG & 8)
+            score = static_cast<float>(q) * a.s2;
+        else if (a.flavor == 0)  // SimdFeatureScorer.cc:142: 0.5 * q / scalingSquared_ in double
             score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
         else  // BatchFeatureScorer.cc:468: (f32)best / scale_
             score = __fdiv_rn(static_cast<float>(q), a.batchScale);
@@ -418,6 +424,8 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
 
     const uint32_t sh   = static_cast<uint32_t>(ib + 1);
     const auto     pack = [&](int acc, int p) {
+        if constexpr ((GMM_I8_DIAG & 2) != 0)
+            return acc;
         return static_cast<int>((static_cast<uint32_t>(acc) << sh) + static_cast<uint32_t>(p));
     };
     // candidate key: the packed value; PRESEL: biased, OR the mask byte of column block cb
@@ -453,7 +461,8 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
             emitMixtureI8<NF>(a, scores, bestOut, unb, mm, frame0, lane, g, ib, ssOut);
         }
         else {
-            emitMixtureI8<NF>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
+            if (!(GMM_I8_DIAG & 4) || mm + 1 == m1)
+                emitMixtureI8<NF>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
         }
     };
     resetBest();

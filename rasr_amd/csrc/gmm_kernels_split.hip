@@ -42,6 +42,9 @@
 #ifndef GMM_SPLIT_MIN_WAVES
 #define GMM_SPLIT_MIN_WAVES 1
 #endif
+#ifndef GMM_SPLIT_IL
+#define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
+#endif
 
 namespace rasr_gmm {
 namespace dev {
@@ -372,7 +375,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     // one pipeline step: the MFMAs of the pair in (A0, A1) into cur beside the epilogue of the pair in
     // prev, interleaved 1 MFMA : 2 VALU (the operand loads for two pairs ahead follow, then finish())
     // (PRESEL: the mask words of the pair in (C0w, C1w) are read into TTcur; TTprev are prev's)
-    constexpr int kIl = PRESEL ? 28 : 24, kIlV = PRESEL ? 3 : 2;
+    constexpr int kIl = PRESEL ? 28 : GMM_SPLIT_IL, kIlV = PRESEL ? 3 : 2;
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
                           const f32x4(&prev)[2][NF], uint32_t tPrev, const uint2& C0w, const uint2& C1w,
                           uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) {

@@ -39,12 +39,12 @@ def main():
                 dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
     t = sum(dur) / len(dur) if dur else float("nan")
-    import hashlib
-    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rasr_amd", "lib", "librasr_gmm.so")
-    with open(lib, "rb") as f:
-        lib_sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from rasr_amd import _capi
+    kernel_id = _capi.load_library().gmm_kernel_id().decode()
     out = {"kernel": args.kernel, "dispatches_per_pass": len(vals.get("SQ_WAVES", [])), "avg_duration_s": t,
-           "library_sha": lib_sha, "frames_per_launch": args.frames_per_launch, "counters": avg}
+           "kernel_id": kernel_id, "frames_per_launch": args.frames_per_launch, "counters": avg}
     if "GRBM_GUI_ACTIVE" in avg:
         out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / t / 1e9
     if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:

@@ -11,26 +11,25 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(args, extra_env=None):
+def _run(args, probe_dir):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env["RASR_BENCH_LAUNCH_PROBE"] = "1"
-    env.update(extra_env or {})
-    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
-                          env=env, timeout=240)
+    env["RASR_BENCH_LAUNCH_PROBE"] = str(probe_dir)  # every rank writes rank<R>.json there
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       env=env, timeout=240)
+    recs = [json.loads(p.read_text()) for p in sorted(probe_dir.glob("rank*.json"))]
+    return r, recs
 
 
 @pytest.mark.parametrize("n", [2, 3])
-def test_launcher_starts_n_ranks(n):
-    r = _run(["--gpus", str(n), "--steps", "1", "--warmup", "0"])
+def test_launcher_starts_n_ranks(n, tmp_path):
+    r, recs = _run(["--gpus", str(n), "--steps", "1", "--warmup", "0"], tmp_path)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-    assert sorted(x["rank"] for x in lines) == list(range(n))
-    assert all(x["world_size"] == n and x["gpus"] == n for x in lines)
-    assert sorted(x["local_rank"] for x in lines) == list(range(n))
+    assert sorted(x["rank"] for x in recs) == list(range(n))
+    assert all(x["world_size"] == n and x["gpus"] == n for x in recs)
+    assert sorted(x["local_rank"] for x in recs) == list(range(n))
 
 
-def test_single_gpu_runs_in_process():
-    r = _run(["--gpus", "1"])
+def test_single_gpu_runs_in_process(tmp_path):
+    r, recs = _run(["--gpus", "1"], tmp_path)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-    assert lines == [{"rank": 0, "world_size": 1, "local_rank": 0, "gpus": 1}]
+    assert recs == [{"rank": 0, "world_size": 1, "local_rank": 0, "gpus": 1}]
