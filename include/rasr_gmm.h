@@ -118,6 +118,11 @@ int      gmm_scorer_type_of(const gmm_scorer* scorer);
  *   scores       [n_mixtures][score_stride] f32: ContextScorer::score(e) per frame
  *   best_density [n_mixtures][score_stride] u32 or NULL: AssigningContextScorer::bestDensity(e)
  *                (batch types have no assignment and ignore it).
+ *                Quantized types: bit-exact (lowest index on equal scores, the reference's strict `<`).
+ *                Float types: the kernel orders candidates by the f32 score with its low 6-8 mantissa bits
+ *                replaced by a (tile, row) tag, so two densities whose scores agree within ~2^-16
+ *                relative may be reported in either order (the lower index wins exact ties); the score
+ *                itself stays within the 1e-4 contract.
  * Replaces per-frame Context construction + calculateScoreAndDensity
  * (SimdFeatureScorer.cc:22-35,135-176) and BatchFeatureScorerBase::fillScoreCache
  * (BatchFeatureScorer.cc:98-105). */

@@ -58,6 +58,21 @@ def test_nn_scorer_gpu(gpu, act, dims, frames):
 
 
 @pytest.mark.gpu
+def test_nn_scorer_bench_shape(gpu):
+    """BASELINE config 5's network exactly as bench.py --mode nn builds it (429 -> 2048 x 6 -> 5000, sigmoid),
+    on a frame count that is not a multiple of the 256-frame tile; checked against the bf16 contract."""
+    dims = [429] + [2048] * 6 + [5000]
+    layers = nn.synthetic_network(dims, "sigmoid", seed=5)
+    x = ra.synthetic_frames(300, 429, seed=6)
+    lp = np.log(np.random.Generator(np.random.PCG64(7)).dirichlet(np.ones(5000))).astype(np.float32)
+    sc = nn.NnScorer(layers, log_prior=lp, prior_scale=0.7, max_frames=512)
+    s = sc.score_host(x)
+    e16 = _err(s, nn_oracle.forward_bf16(layers, x, lp, 0.7).astype(np.float64))
+    print(f"bench shape: vs bf16 contract {e16:.2e}")
+    assert e16 <= 2e-3
+
+
+@pytest.mark.gpu
 def test_nn_scorer_device_strides_and_errors(gpu):
     import torch
     layers = nn.synthetic_network([39, 300, 200], "sigmoid", seed=9)
