@@ -30,7 +30,11 @@
 
 #ifndef GMM_I8_DIAG
 #define GMM_I8_DIAG 0  // timing diagnostics only (wrong results): 2 = keys without the pack, 4 = emit only the
-                       // chunk's last mixture, 8 = f32 finalize instead of the f64 division
+                       // chunk's last mixture, 8 = f32 finalize instead of the f64 division, 16 = every step
+                       // reads the segment's first tiles (loop-invariant LDS reads)
+#endif
+#ifndef GMM_I8_EXTRA_LDS
+#define GMM_I8_EXTRA_LDS 0  // A/B only: dynamic LDS bytes added to scoreI8Seg's workgroup (limits workgroups per CU)
 #endif
 #ifndef GMM_I8_INTERLEAVE
 #define GMM_I8_INTERLEAVE 4  // VALU per MFMA in a sched_group_barrier interleave of the pair step (0 = off; 4: +2 %, 6: -4 %)
@@ -315,7 +319,10 @@ __global__ __launch_bounds__(256) void scoreI8(I8Args a) {
 // the segment after next.  Mixture boundaries are independent of segment
 // boundaries.
 // ---------------------------------------------------------------------------
-constexpr int kSegTiles = 8;
+#ifndef GMM_I8_SEG
+#define GMM_I8_SEG 16  // tiles per LDS segment (A/B at 32768 frames: 16 -1.2 % vs 8, 4 +1.6 %; kTilePad >= SEG)
+#endif
+constexpr int kSegTiles = GMM_I8_SEG;
 
 // preselection-batch-int: the segment ring and the waves' mask tables share one dynamic LDS array
 extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
@@ -488,7 +495,7 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
         const uint32_t segEnd = min(segT0 + kSegTiles, T1);
         uint32_t       t      = segT0;
         while (t < segEnd) {
-            const uint32_t lt = t - segT0;
+            const uint32_t lt = (GMM_I8_DIAG & 16) ? 0u : t - segT0;
             if (t + 1 < segEnd && t + 1 < tEnd) {
                 // two tiles of the same mixture: 2 NF independent MFMAs, one v_min3 per candidate pair
                 i32x4 A0[KS], A1[KS];
@@ -597,7 +604,9 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
                                a.mixTileOff, a.scores, a.best);
             return;
         }
-        hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS>), dim3(grid), dim3(256), 0, s, a, a.mixTileOff, a.scores, a.best);
+        // 16-tile segments for one K step (34 KiB per workgroup, 4 per CU); 8 for two (also 34 KiB)
+        hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS, false, (KS == 1 ? dev::kSegTiles : 8)>), dim3(grid), dim3(256),
+                           GMM_I8_EXTRA_LDS, s, a, a.mixTileOff, a.scores, a.best);
         return;
     }
 #endif
