@@ -639,21 +639,27 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
 // With u the MFMA value (2 s + K0, times 2^-e) and kap = 0.5 log2(e) 2^e of the frame,
 // exp(-s_d) = exp(K0/2) 2^(-kap u_d), so every lane keeps, per column block, a reference R (on the
 // kap u scale) and per slot S = sum 2^(R - kap u): one v_fma + v_exp + v_add per value beside the
-// (tag, min) key of diagonal-maximum.  R is re-based (a uniform branch, rare after the first pair of
-// a mixture) whenever a new value would put an exponent above 64; the final score is
-// R ln2 - K0/2 - ln(S) after the (R, S) pairs of the four lane groups are merged on a common R.
-// 16-row tiles, tile pairs, operands two pairs ahead as scoreSplit; no MFMA/VALU interleave.
+// (tag, min) key of diagonal-maximum.  R is re-based (a uniform branch, taken at the first tile of a
+// mixture and rarely after) whenever the smallest value so far would put an exponent above 64; the
+// final score is R ln2 - K0/2 - ln(S) after the (R, S) pairs of the four lane groups are merged on a
+// common R.
+//
+// Software pipeline per 16-row tile: step t issues the KS x NF MFMAs of tile t beside the epilogue of
+// tile t-1, in two halves around the re-base branch -- keys + min and the re-base test beside the first
+// KS/2 k-steps, the exponentials and sums beside the rest -- then emits the mixture tile t-1 ended, if
+// any.  Two slots per column block (a key carries its row, so any slot may hold any row).  Operands of
+// four consecutive tiles in flight (R0..R3), accumulators alternate between two sets.
 // ---------------------------------------------------------------------------
 template <bool BEST>
-__device__ __forceinline__ void emitMixtureSplitSum(const SplitArgs& a, const uint32_t (&best)[4][4],
-                                                    const float (&S)[4][4], const float (&R)[4], uint32_t m,
+__device__ __forceinline__ void emitMixtureSplitSum(const SplitArgs& a, const uint32_t (&best)[4][2],
+                                                    const float (&S)[4][2], const float (&R)[4], uint32_t m,
                                                     uint32_t frame0, int lane, uint32_t g, uint32_t kmask) {
     uint32_t k[4];
     float    sum[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
-        k[cb]   = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
-        sum[cb] = (S[cb][0] + S[cb][1]) + (S[cb][2] + S[cb][3]);
+        k[cb]   = min(best[cb][0], best[cb][1]);
+        sum[cb] = S[cb][0] + S[cb][1];
     }
     // merge (R, S) of two lane groups on the smaller R
     const auto merge = [](float ra, float sa, float rb, float sb, float& r, float& sm) {
@@ -705,6 +711,7 @@ template <int KS, bool BEST>
 __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(SplitArgs a,
                                                                          const uint32_t* __restrict__ mixTileOff) {
     constexpr int  NF   = 4;
+    constexpr int  KH   = KS / 2;  // k-steps issued beside the first half of the epilogue
     const int      lane = threadIdx.x & 63;
     const int      wave = threadIdx.x >> 6;
     const uint32_t g    = static_cast<uint32_t>(lane) >> 4;
@@ -739,6 +746,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             asm volatile("" ::"v"(B[cb][s]));
         asm volatile("" ::"v"(kap[cb]));
     }
+    // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
     f16x8 R0[KS], R1[KS], R2[KS], R3[KS];
     loadTile(T0, R0);
     loadTile(T0 + 1, R1);
@@ -749,78 +757,19 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     uint32_t       vmask = ~kmask;
     asm volatile("" : "+v"(vmask));
 
-    uint32_t   best[NF][4];
-    float      S[NF][4], Rf[NF];
+    uint32_t   best[NF][2];
+    float      S[NF][2], Rf[NF];
     const auto resetBest = [&]() {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb) {
-            Rf[cb] = 1e30f;  // no reference yet: the first values re-base it
+            Rf[cb] = 1e30f;  // no reference yet: the first tile re-bases it
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                best[cb][r] = 0xffffffffu;
-                S[cb][r]    = 0.0f;
+            for (int h = 0; h < 2; ++h) {
+                best[cb][h] = 0xffffffffu;
+                S[cb][h]    = 0.0f;
             }
         }
     };
-    const auto chain = [&](const f16x8(&A)[KS], f32x4(&acc)[NF]) {
-#pragma unroll
-        for (int cb = 0; cb < NF; ++cb)
-            acc[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-            for (int cb = 0; cb < NF; ++cb)
-                acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
-    };
-    const auto pairStep = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], uint32_t tl) {
-        f32x4 acc[2][NF];
-        chain(A0, acc[0]);
-        chain(A1, acc[1]);
-        uint32_t tagA[4], tagB[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            tagA[r] = (tl << 2) | r;
-            tagB[r] = ((tl + 1u) << 2) | r;
-            asm("" : "+s"(tagA[r]), "+s"(tagB[r]));
-        }
-        float t[2][NF][4];
-        bool  rebase = false;
-#pragma unroll
-        for (int cb = 0; cb < NF; ++cb) {
-            float tmx = -3.40282347e+38f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t ka = (__float_as_uint(acc[0][cb][r]) & vmask) | tagA[r];
-                const uint32_t kb = (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
-                best[cb][r]       = umin3(best[cb][r], ka, kb);
-                t[0][cb][r]       = __builtin_fmaf(acc[0][cb][r], -kap[cb], Rf[cb]);
-                t[1][cb][r]       = __builtin_fmaf(acc[1][cb][r], -kap[cb], Rf[cb]);
-                tmx               = fmaxf(tmx, fmaxf(t[0][cb][r], t[1][cb][r]));
-            }
-            rebase = rebase || tmx > 64.0f;
-        }
-        if (__builtin_amdgcn_ballot_w64(rebase) != 0) {  // uniform: new reference R = kap * (best value so far)
-#pragma unroll
-            for (int cb = 0; cb < NF; ++cb) {
-                const uint32_t kb = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
-                const float    nr = kap[cb] * __uint_as_float(kb & vmask);
-                const float    f  = __builtin_amdgcn_exp2f(nr - Rf[cb]);
-                Rf[cb]            = nr;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    S[cb][r]    = S[cb][r] * f;
-                    t[0][cb][r] = __builtin_fmaf(acc[0][cb][r], -kap[cb], nr);
-                    t[1][cb][r] = __builtin_fmaf(acc[1][cb][r], -kap[cb], nr);
-                }
-            }
-        }
-#pragma unroll
-        for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                S[cb][r] += __builtin_amdgcn_exp2f(t[0][cb][r]) + __builtin_amdgcn_exp2f(t[1][cb][r]);
-    };
-
     uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
     const auto emit    = [&]() { emitMixtureSplitSum<BEST>(a, best, S, Rf, m, frame0, lane, g, kmask); };
@@ -834,6 +783,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
         }
     };
+    // after the epilogue of the tile that ends at tNext
     const auto finish = [&](uint32_t tNext) {
         if (tNext == tEnd) {
             emit();
@@ -841,25 +791,151 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             advance(tNext);
         }
     };
-    while (m < m1 && tEnd == T0) {
+
+    // keys + min of tile tPrev (values prev) and the re-base test, beside MFMA k-steps [0, KH) into cur
+    const auto firstHalf = [&](const f16x8(&A)[KS], f32x4(&cur)[NF], const f32x4(&prev)[NF], uint32_t tPrev) -> bool {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+            cur[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < KH; ++s)
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                cur[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], cur[cb], 0, 0, 0);
+        const uint32_t tl = tPrev - tBeg;
+        uint32_t       tag[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            tag[r] = (tl << 2) | static_cast<uint32_t>(r);
+            asm("" : "+s"(tag[r]));  // opaque: one v_and_or_b32 per key
+        }
+        bool reb = false;
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            const uint32_t k0 = (__float_as_uint(prev[cb][0]) & vmask) | tag[0];
+            const uint32_t k1 = (__float_as_uint(prev[cb][1]) & vmask) | tag[1];
+            const uint32_t k2 = (__float_as_uint(prev[cb][2]) & vmask) | tag[2];
+            const uint32_t k3 = (__float_as_uint(prev[cb][3]) & vmask) | tag[3];
+            best[cb][0]       = umin3(best[cb][0], k0, k1);
+            best[cb][1]       = umin3(best[cb][1], k2, k3);
+            const float vmin  = __uint_as_float(min(best[cb][0], best[cb][1]) & vmask);
+            reb               = reb || __builtin_fmaf(vmin, -kap[cb], Rf[cb]) > 64.0f;
+        }
+        constexpr int kM1 = KH * NF;
+        if constexpr (kM1 > 0) {
+#pragma unroll
+            for (int i = 0; i < kM1; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // VALU
+            }
+        }
+        return reb;
+    };
+    // the exponentials and sums of tile tPrev, beside MFMA k-steps [KH, KS) into cur
+    const auto secondHalf = [&](const f16x8(&A)[KS], f32x4(&cur)[NF], const f32x4(&prev)[NF]) {
+#pragma unroll
+        for (int s = KH; s < KS; ++s)
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                cur[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], cur[cb], 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                S[cb][h] += __builtin_amdgcn_exp2f(__builtin_fmaf(prev[cb][2 * h], -kap[cb], Rf[cb])) +
+                            __builtin_amdgcn_exp2f(__builtin_fmaf(prev[cb][2 * h + 1], -kap[cb], Rf[cb]));
+#pragma unroll
+        for (int i = 0; i < (KS - KH) * NF; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // VALU
+        }
+    };
+    const auto rebase = [&]() {  // uniform: new reference R = kap * (best value so far)
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            const float nr = kap[cb] * __uint_as_float(min(best[cb][0], best[cb][1]) & vmask);
+            const float f  = __builtin_amdgcn_exp2f(nr - Rf[cb]);
+            Rf[cb]         = nr;
+            S[cb][0] *= f;
+            S[cb][1] *= f;
+        }
+    };
+    // step: MFMAs of the tile in A into cur beside the epilogue of tile tPrev (prev); then its emit
+    const auto step = [&](const f16x8(&A)[KS], f32x4(&cur)[NF], const f32x4(&prev)[NF], uint32_t tPrev) {
+        if (__builtin_amdgcn_ballot_w64(firstHalf(A, cur, prev, tPrev)) != 0)
+            rebase();
+        secondHalf(A, cur, prev);
+    };
+    // the last tile's epilogue (no MFMAs left to issue beside it)
+    const auto drain = [&](const f32x4(&prev)[NF], uint32_t tPrev) {
+        const uint32_t tl = tPrev - tBeg;
+        bool           reb = false;
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            uint32_t k[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                k[r] = (__float_as_uint(prev[cb][r]) & vmask) | ((tl << 2) | static_cast<uint32_t>(r));
+            best[cb][0]      = umin3(best[cb][0], k[0], k[1]);
+            best[cb][1]      = umin3(best[cb][1], k[2], k[3]);
+            const float vmin = __uint_as_float(min(best[cb][0], best[cb][1]) & vmask);
+            reb              = reb || __builtin_fmaf(vmin, -kap[cb], Rf[cb]) > 64.0f;
+        }
+        if (__builtin_amdgcn_ballot_w64(reb) != 0)
+            rebase();
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                S[cb][h] += __builtin_amdgcn_exp2f(__builtin_fmaf(prev[cb][2 * h], -kap[cb], Rf[cb])) +
+                            __builtin_amdgcn_exp2f(__builtin_fmaf(prev[cb][2 * h + 1], -kap[cb], Rf[cb]));
+        finish(tPrev + 1);
+    };
+
+    while (m < m1 && tEnd == T0) {  // mixtures without tiles at the start of the chunk
         emit();
         ++m;
         tEnd = m < m1 ? mixTileOff[m + 1] : T0;
     }
-    uint32_t t = T0;
-    for (; t + 4 <= T1; t += 4) {
-        pairStep(R0, R1, t - tBeg);
-        loadTile(t + 4, R0);
-        loadTile(t + 5, R1);
-        finish(t + 2);
-        pairStep(R2, R3, t + 2 - tBeg);
-        loadTile(t + 6, R2);
-        loadTile(t + 7, R3);
-        finish(t + 4);
-    }
-    if (t < T1) {
-        pairStep(R0, R1, t - tBeg);
-        finish(t + 2);
+    if (T0 < T1) {
+        // T1 - T0 is even: after the first tile, whole groups of four steps, then one or three more
+        f32x4 accX[NF], accY[NF];
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            accX[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                accX[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(R0[s], B[cb][s], accX[cb], 0, 0, 0);
+        }
+        loadTile(T0 + 4, R0);
+        uint32_t t = T0;  // tile whose values are in accX
+        for (; t + 4 < T1; t += 4) {
+            step(R1, accY, accX, t);
+            loadTile(t + 5, R1);
+            finish(t + 1);
+            step(R2, accX, accY, t + 1);
+            loadTile(t + 6, R2);
+            finish(t + 2);
+            step(R3, accY, accX, t + 2);
+            loadTile(t + 7, R3);
+            finish(t + 3);
+            step(R0, accX, accY, t + 3);
+            loadTile(t + 8, R0);
+            finish(t + 4);
+        }
+        // T1 - 1 - t is 1 or 3
+        step(R1, accY, accX, t);
+        finish(t + 1);
+        if (t + 2 < T1) {
+            step(R2, accX, accY, t + 1);
+            finish(t + 2);
+            step(R3, accY, accX, t + 2);
+            finish(t + 3);
+            drain(accY, t + 3);
+        }
+        else {
+            drain(accY, t + 1);
+        }
     }
 }
 
