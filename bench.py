@@ -57,6 +57,9 @@ PEAK_F16_MFMA_TFLOPS = 2516.6         # v_mfma_f32_16x16x32_f16, dense (same rat
 PEAK_I8_MFMA_TOPS = 2 * 2516.6        # i8 MFMA = 2x the bf16 dense rate
 SPLIT_PRODUCTS = 3                    # split-f16 kernel: mh*xh + mh*xl + ml*xh per f32 multiply-add
 CPU_SHARE_PER_GPU = 16                # host CPUs a one-GPU box grants this job
+N_SIMDS = 256 * 4                     # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4                       # peak engine clock the MFMA peaks are quoted at
+VOP3_CYCLES = 3.14                    # measured issue cost of a 3-source VOP3 per SIMD (profiles/r02/vgpr_banks.txt)
 
 MODES = {
     "fp32": ("diagonal-maximum", "f32"),
@@ -292,6 +295,18 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
             "output_bytes_per_launch": m_local * fpl * (4 + (0 if best is None else 4)),
         },
     }
+    if kernel.startswith("scoreI8"):
+        # the quantized scorer is reported against max(t_MFMA, t_VALU).  Its epilogue is one
+        # 3-source VOP3 (v_lshl_add) per (frame, density) plus half a v_min3; a wave64 VOP3 issues every
+        # VOP3_CYCLES cycles per SIMD with 4 waves per SIMD (scripts/debug/vgpr_banks.hip)
+        keys_per_s = N_SIMDS * CLOCK_GHZ * 1e9 * 64.0 / (1.5 * VOP3_CYCLES)
+        ceiling = keys_per_s / d_local
+        res["roofline"]["valu"] = {
+            "ceiling_frames_per_s": ceiling,
+            "frac": (fpl / sec) / ceiling,
+            "basis": f"1.5 VOP3 per (frame, density), {VOP3_CYCLES} cycles per wave64 VOP3 per SIMD, "
+                     f"{N_SIMDS} SIMDs at {CLOCK_GHZ} GHz",
+        }
     del sc, scores, best, frames
     torch.cuda.empty_cache()
     return res

@@ -29,6 +29,9 @@ for s in $STEPS; do
          step pmc_simd 900 bash scripts/profile_pmc.sh simd &&
          python scripts/pmc_summary.py $OUT/pmc_fp32 scoreSplit --json $OUT/pmc_fp32.json > /dev/null &&
          python scripts/pmc_summary.py $OUT/pmc_simd scoreI8 --json $OUT/pmc_simd.json > /dev/null ;;
+    sweep) step sweep 1200 bash scripts/sweep_batch.sh ;;
+    bench_sum) step bench_sum 600 python bench.py --mode sum --steps 20 --warmup 3 --cpu-baseline off --host-boundary off --no-extra-mode ;;
+    bench_nn) step bench_nn 600 python bench.py --mode nn --steps 20 --warmup 3 ;;
     pytest_new) step pytest_new 1200 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $PYTEST_ARGS ;;
   esac
 done
