@@ -22,6 +22,7 @@ namespace dev {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float  f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef float  f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float activate(float x, int act, float gamma) {
     switch (act) {
@@ -380,6 +381,9 @@ __global__ __launch_bounds__(512) void nnGemm256(NnGemmArgs a) {
 #ifndef NN8_EARLY
 #define NN8_EARLY 0  // 1: both halves of tile v+1 still missing are staged in p1 (3 phases before the wait)
 #endif
+#ifndef NN8_MFMA32
+#define NN8_MFMA32 0  // 1: each quadrant on v_mfma_f32_32x32x16_bf16 (2 blocks of 32 x 32, 8 MFMAs) instead of 16x16x32
+#endif
 #ifndef NN8_PRIO_MODE
 #define NN8_PRIO_MODE 2  // 0: s_setprio(1) around each MFMA cluster; 1: once for group 1; 2: none (fastest, A/B)
 #endif
@@ -419,15 +423,59 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
                                                 (c ^ nnSwz(row)) * 8u);
     };
     const uint32_t rl = static_cast<uint32_t>(lane) & 15u;
+#if NN8_MFMA32
+    // 32 x 32 blocks: lane l holds row (l & 31), k = 16 s + 8 (l >> 5) + 0..7 of A and B (16-byte piece
+    // 2 s + (l >> 5)); accumulator register i = row (i & 3) + 8 (i >> 2) + 4 (l >> 5), column l & 31
+    const uint32_t r32 = static_cast<uint32_t>(lane) & 31u, h32 = static_cast<uint32_t>(lane) >> 5;
+    const auto     frag32 = [&](uint32_t buf, int op, uint32_t row, uint32_t s) {
+        const uint32_t c = 2u * s + h32;
+        return *reinterpret_cast<const bf16x8*>(nnLds + (buf * 2u + static_cast<uint32_t>(op)) * kOp + row * BK +
+                                                (c ^ nnSwz(row)) * 8u);
+    };
+    typedef bf16x8 FragA[2][4];
+    typedef bf16x8 FragB[4];
+    const auto readA = [&](uint32_t buf, uint32_t h, FragA& fa) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+                fa[ib][s] = frag32(buf, 0, h * 128u + wr * 64u + 32u * ib + r32, s);
+    };
+    const auto readB = [&](uint32_t buf, uint32_t h, FragB& fb) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            fb[s] = frag32(buf, 1, h * 128u + wc * 32u + r32, s);
+    };
+    f32x16 acc[4][2];  // [2 ha + ib][hb]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            acc[i][j] = f32x16{};
+    const auto quadrant = [&](int ha, int hb, const FragA& fa, const FragB& fb) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        NN8_PRIO(1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+                acc[2 * ha + ib][hb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ib][s], fb[s], acc[2 * ha + ib][hb], 0, 0, 0);
+        NN8_PRIO(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+#else
     // sub-tile reads: A half h -> rows 128 h + 64 wr + 16 i + rl; B half h -> rows 128 h + 32 wc + 16 j + rl
-    const auto readA = [&](uint32_t buf, uint32_t h, bf16x8(&fa)[4][2]) {
+    typedef bf16x8 FragA[4][2];
+    typedef bf16x8 FragB[2][2];
+    const auto readA = [&](uint32_t buf, uint32_t h, FragA& fa) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 fa[i][ks] = frag(buf, 0, h * 128u + wr * 64u + 16u * i + rl, ks);
     };
-    const auto readB = [&](uint32_t buf, uint32_t h, bf16x8(&fb)[2][2]) {
+    const auto readB = [&](uint32_t buf, uint32_t h, FragB& fb) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -441,7 +489,7 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    const auto quadrant = [&](int ha, int hb, const bf16x8(&fa)[4][2], const bf16x8(&fb)[2][2]) {
+    const auto quadrant = [&](int ha, int hb, const FragA& fa, const FragB& fb) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         NN8_PRIO(1);
@@ -456,6 +504,8 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
         NN8_PRIO(0);
         __builtin_amdgcn_sched_barrier(0);
     };
+
+#endif
 
     // prologue: tile 0 whole, A0 / B0 of tile 1; tile 0 retired
     stage(0, 0, 0, 0);
@@ -478,7 +528,8 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
         __builtin_amdgcn_s_setprio(1);  // static form: the younger half keeps priority
 #endif
 
-    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+    FragA fa;
+    FragB fb0, fb1;
     for (uint32_t v = 0; v < nK; ++v) {
         const uint32_t buf = v & 1u;
         const bool     n1 = v + 1 < nK, n2 = v + 2 < nK;
@@ -522,6 +573,36 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
     if (NN8_STAGGER && wr == 0)
         __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
 
+#if NN8_MFMA32
+    // epilogue: block (ha, ib, hb) register 4 q + rr -> row m0 + 128 ha + 64 wr + 32 ib + 8 q + 4 h32 + rr,
+    //           frame n0 + 128 hb + 32 wc + r32
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t n = n0 + 128u * j + wc * 32u + r32;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t mb = m0 + 128u * (i >> 1) + wr * 64u + 32u * (i & 1) + 8u * q + 4u * h32;
+                const f32x4    bs = *reinterpret_cast<const f32x4*>(a.bias + mb);
+                if (a.top) {
+                    if (n < a.nFrames)
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr)
+                            if (mb + rr < a.M)
+                                a.scores[static_cast<size_t>(mb + rr) * a.scoreStride + n] = -(acc[i][j][4 * q + rr] + bs[rr]);
+                }
+                else {
+                    u16x4 v;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        v[rr] = toBf16(activate(acc[i][j][4 * q + rr] + bs[rr], a.act, a.gamma));
+                    *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
+                }
+            }
+        }
+    }
+#else
     // epilogue: rows m = m0 + 128 (i >> 2) + 64 wr + 16 (i & 3) + 4 (lane >> 4) + rr,
     //           frame n = n0 + 128 (j >> 1) + 32 wc + 16 (j & 1) + (lane & 15)
     const uint32_t g = static_cast<uint32_t>(lane) >> 4, col = rl;
@@ -548,6 +629,7 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
             }
         }
     }
+#endif
 }
 
 }  // namespace dev
