@@ -66,8 +66,9 @@ $(BUILD)/nn_api.o: $(SRC)/nn_api.cc $(HDRS)
 
 # identity of the device code (hash of the kernel sources and their flags): profiling summaries record it and
 # bench.py uses a summary only for the kernels it was measured on
-KERNEL_SRCS = $(SRC)/gmm_kernels_i8.hip $(SRC)/gmm_kernels_f32.hip $(SRC)/gmm_kernels_split.hip $(SRC)/gmm_kernels_presel.hip \
-              $(SRC)/gmm_kernels_shard.hip $(SRC)/nn_kernels.hip $(SRC)/gmm_device.hh $(SRC)/gmm_kernels.hh $(SRC)/nn_kernels.hh
+# the GMM scorer kernels the PMC summaries (profiles/pmc_*.json) measure: their sources and flags
+KERNEL_SRCS = $(SRC)/gmm_kernels_i8.hip $(SRC)/gmm_kernels_f32.hip $(SRC)/gmm_kernels_split.hip \
+              $(SRC)/gmm_device.hh $(SRC)/gmm_kernels.hh
 $(BUILD)/kernel_id.h: $(KERNEL_SRCS) Makefile
 	@mkdir -p $(BUILD)
 	@echo "#define GMM_KERNEL_ID \"$$( (cat $(KERNEL_SRCS); echo '$(HIPFLAGS) $(I8FLAGS) $(F32FLAGS) $(SPLITFLAGS)') | sha256sum | cut -c1-16)\"" > $@
