@@ -33,6 +33,9 @@
                        // chunk's last mixture, 8 = f32 finalize instead of the f64 division, 16 = every step
                        // reads the segment's first tiles (loop-invariant LDS reads)
 #endif
+#ifndef GMM_I8_BUFSTORE
+#define GMM_I8_BUFSTORE 1  // emit: buffer stores bounded by num_records instead of a per-lane frame branch
+#endif
 #ifndef GMM_I8_EXTRA_LDS
 #define GMM_I8_EXTRA_LDS 0  // A/B only: dynamic LDS bytes added to scoreI8Seg's workgroup (limits workgroups per CU)
 #endif
@@ -124,22 +127,26 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
 #endif
 
     const uint32_t mo = m;
+#if GMM_I8_BUFSTORE
+    // frames >= nFrames fall outside num_records: the buffer stores drop them (no per-lane branch)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                     static_cast<int>(a.nFrames * 4u), 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc(bestOut ? bestOut + static_cast<size_t>(mo) * a.scoreStride
+                                                              : nullptr,
+                                                     (short)0, static_cast<int>(a.nFrames * 4u), 0x00020000);
+#endif
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
         const uint32_t f = frame0 + 64 * i + lane;
+#if !GMM_I8_BUFSTORE
         if (f >= a.nFrames)
             continue;
+#endif
         const int packed = res[i];
-        int       q;
-        uint32_t  dns;
-        if (packed == INT_MAX) {  // mixture without densities: minScore stays Core::Type<int>::max
-            q   = INT_MAX;
-            dns = 0xffffffffu;
-        }
-        else {
-            q   = (packed >> ib) + ssOut[i];
-            dns = static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
-        }
+        // mixture without densities: minScore stays Core::Type<int>::max
+        const bool     none = packed == INT_MAX;
+        const int      q    = none ? INT_MAX : (packed >> ib) + ssOut[i];
+        const uint32_t dns  = none ? 0xffffffffu : static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
         float score;
         if (GMM_I8_DIAG & 8)
             score = static_cast<float>(q) * a.s2;
@@ -149,10 +156,16 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
             score = __fdiv_rn(static_cast<float>(q), a.batchScale);
         if (a.outScale != 1.0f)
             score = __fmul_rn(a.outScale, score);  // ScaledContextScorer::score, ScaledFeatureScorer.hh:62-64
+#if GMM_I8_BUFSTORE
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, f * 4u, 0, 0);
+        if (bestOut)
+            __builtin_amdgcn_raw_buffer_store_b32(dns, rb, f * 4u, 0, 0);
+#else
         const size_t o = static_cast<size_t>(mo) * a.scoreStride + f;
         scores[o]      = score;
         if (bestOut)
             bestOut[o] = dns;
+#endif
     }
 }
 
