@@ -285,6 +285,11 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.idxBits     = s->idxBits;
         a.flavor      = s->flavor == Flavor::Simd ? 0 : 1;
         a.s2          = s->scalingSquared;
+        // SIMD finalize by multiplication (gmm_kernels_i8.hip, emitMixtureI8); scales far outside a real
+        // model's range keep the division
+        a.halfInvS2 = (s->scalingSquared >= 1e-30f && s->scalingSquared <= 1e30f)
+                              ? 0.5 * (1.0 / static_cast<double>(s->scalingSquared))
+                              : 0.0;
         a.batchScale  = s->batchScale;
         a.outScale    = s->cfg.score_scale;
         a.presel      = s->presel ? 1 : 0;

@@ -36,6 +36,7 @@ struct I8Args {
     uint32_t        idxBits;
     int             flavor;       // 0 SIMD-diagonal-maximum, 1 batch-int
     float           s2, batchScale, outScale;
+    double          halfInvS2;    // 0.5 * RN64(1 / s2) for the SIMD finalize, 0 = always divide (gmm_kernels_i8.hip)
     // preselection-batch-int (gmm_kernels_presel.hip): per-(frame, cluster) mask, per-row cluster offsets
     const uint32_t* selT;         // [nFramesPad/64][nClusters][16] u32, byte (frame%64)/16 = 0xff: deselected
     const void*     tileClu;      // u16 [T+pad][16]: cluster * 64 (byte offset into a wave's mask table)

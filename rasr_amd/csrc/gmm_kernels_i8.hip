@@ -33,6 +33,9 @@
                        // chunk's last mixture, 8 = f32 finalize instead of the f64 division, 16 = every step
                        // reads the segment's first tiles (loop-invariant LDS reads)
 #endif
+#ifndef GMM_I8_FASTDIV
+#define GMM_I8_FASTDIV 1  // SIMD finalize: multiply by the double reciprocal, divide only next to an f32 midpoint
+#endif
 #ifndef GMM_I8_BUFSTORE
 #define GMM_I8_BUFSTORE 1  // emit: buffer stores bounded by num_records instead of a per-lane frame branch
 #endif
@@ -150,8 +153,22 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
         float score;
         if (GMM_I8_DIAG & 8)
             score = static_cast<float>(q) * a.s2;
-        else if (a.flavor == 0)  // SimdFeatureScorer.cc:142: 0.5 * q / scalingSquared_ in double
+        else if (a.flavor == 0) {  // SimdFeatureScorer.cc:142: (f32)(0.5 * q / scalingSquared_) in double
+#if GMM_I8_FASTDIV
+            // y = q * 0.5 RN64(1/s2) is within 3 ulp of the exact quotient, so (f32)y equals (f32) of the
+            // correctly rounded double quotient unless an f32 rounding midpoint (the 29 bits below f32
+            // precision = 2^28) lies within 4 ulp of y: then the division itself (never, in practice:
+            // tests/test_fastdiv_finalize.py)
+            const double   y  = static_cast<double>(q) * a.halfInvS2;
+            const uint32_t lo = static_cast<uint32_t>(__double_as_longlong(y)) & 0x1fffffffu;
+            if (a.halfInvS2 == 0.0 || lo - (0x10000000u - 4u) <= 8u)
+                score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
+            else
+                score = static_cast<float>(y);
+#else
             score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
+#endif
+        }
         else  // BatchFeatureScorer.cc:468: (f32)best / scale_
             score = __fdiv_rn(static_cast<float>(q), a.batchScale);
         if (a.outScale != 1.0f)
