@@ -89,6 +89,8 @@ def parse():
     p.add_argument("--mixtures", type=int, default=5000)
     p.add_argument("--densities", type=int, default=160)
     p.add_argument("--dim", type=int, default=39)
+    p.add_argument("--ragged", action="store_true",
+                   help="SURVEY 8(d) ragged variant: K_m ~ U[64, 256] with the same total of densities")
     p.add_argument("--no-best", action="store_true", help="do not write best-density indices")
     p.add_argument("--no-extra-mode", action="store_true", help="do not time the other mode")
     p.add_argument("--native-f32", action="store_true",
@@ -478,7 +480,8 @@ def main():
             import torch.distributed as dist
             dist.destroy_process_group()
         return
-    ms = ra.synthetic_mixture_set(args.mixtures, args.densities, args.dim, seed=2024)
+    counts = (ra.ragged_counts(args.mixtures, args.mixtures * args.densities) if args.ragged else args.densities)
+    ms = ra.synthetic_mixture_set(args.mixtures, counts, args.dim, seed=2024)
     res = run_mode(args, args.mode, ms, ws, rank, local, launches)
     extra = {}
     if not args.no_extra_mode:
@@ -514,7 +517,7 @@ def main():
                             f"batched frames",
                 "scorer": MODES[args.mode][0],
                 "mixtures": args.mixtures,
-                "densities_per_mixture": args.densities,
+                "densities_per_mixture": "U[64, 256] (ragged, same total)" if args.ragged else args.densities,
                 "dimension": args.dim,
                 "frames_per_gpu_per_step": res["frames_per_step"],
                 "frames_per_launch": res["frames_per_launch"],

@@ -1,4 +1,4 @@
-// gmm_kernels.hip -- MI355X (gfx950) kernels of the diagonal-GMM feature scorer.
+// gmm_kernels_i8.hip -- MI355X (gfx950) kernels of the diagonal-GMM feature scorer: the quantized ones.
 //
 // Hot path: for a batch of F frames and every mixture e of the model,
 //   score(e,t) = min_{d in e} [ c_d + || A_d - x_t ||^2 ]   (+ argmin)
@@ -9,12 +9,13 @@
 // the matrix cores and the per-mixture minimum is a running min in the MFMA
 // accumulator registers, reduced across the wave once per mixture:
 //
-//   quantized (SIMD-diagonal-maximum, batch-int): v_mfma_i32_16x16x64_i8 on
-//     s8 operands (q - 128); exact integer arithmetic; epilogue per element is
+//   quantized (SIMD-diagonal-maximum, batch-int; this file): v_mfma_i32_16x16x64_i8
+//     on s8 operands (q - 128); exact integer arithmetic; epilogue per element is
 //     one v_lshl_add (constant + 2*dot, packed with the density index in the
-//     low bits) and one v_min_i32 -> bit-identical scores and argmins;
-//   float (diagonal-maximum, batch-float): v_mfma_f32_16x16x4_f32, the row
-//     constant folded into one K column; epilogue v_cmp + 2 v_cndmask.
+//     low bits) and half a v_min3_i32 -> bit-identical scores and argmins;
+//   float (diagonal-maximum, batch-float, diagonal-sum): gmm_kernels_split.hip
+//     (f32 operands as two f16 pieces on the f16 matrix cores) and
+//     gmm_kernels_f32.hip (v_mfma_f32_16x16x4_f32).
 //
 // Work decomposition: one 256-thread workgroup = 4 waves x NF column blocks of
 // 16 frames; it walks a chunk of consecutive mixtures (all their tiles of 16

@@ -30,6 +30,8 @@ for s in $STEPS; do
          python scripts/pmc_summary.py $OUT/pmc_fp32 scoreSplit --json $OUT/pmc_fp32.json > /dev/null &&
          python scripts/pmc_summary.py $OUT/pmc_simd scoreI8 --json $OUT/pmc_simd.json > /dev/null ;;
     sweep) step sweep 1200 bash scripts/sweep_batch.sh ;;
+    bench_d45) step bench_d45 600 python bench.py --dim 45 --steps 20 --warmup 3 --cpu-baseline off --host-boundary off ;;
+    bench_ragged) step bench_ragged 600 python bench.py --ragged --steps 20 --warmup 3 --cpu-baseline off --host-boundary off ;;
     bench_sum) step bench_sum 600 python bench.py --mode sum --steps 20 --warmup 3 --cpu-baseline off --host-boundary off --no-extra-mode ;;
     bench_nn) step bench_nn 600 python bench.py --mode nn --steps 20 --warmup 3 ;;
     pytest_new) step pytest_new 1200 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $PYTEST_ARGS ;;
