@@ -22,7 +22,8 @@ HDRS      = include/rasr_gmm.h $(SRC)/gmm_presel.hh $(SRC)/gmm_prepare.hh $(SRC)
 LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
             $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/MixtureSetEstimatorFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
-            $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o $(BUILD)/gmm_kernels_shard.o $(BUILD)/gmm_hostio.o
+            $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o $(BUILD)/gmm_kernels_shard.o $(BUILD)/gmm_hostio.o \
+            $(BUILD)/gmm_kernels_direct.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 REFSORT   = $(BUILD)/tests/refsort_test
@@ -45,6 +46,12 @@ $(BUILD)/gmm_kernels_split.o: $(SRC)/gmm_kernels_split.hip $(HDRS)
 $(BUILD)/gmm_kernels_presel.o: $(SRC)/gmm_kernels_presel.hip $(SRC)/gmm_refsort.hh $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# reference-order float scorers (GMM_FLAG_REFERENCE_ORDER): scalar f32 ops in the reference's order
+# (no SLP packing into v_pk_*_f32, which issue at a third of the scalar VOP2 rate)
+$(BUILD)/gmm_kernels_direct.o: $(SRC)/gmm_kernels_direct.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 
 # density-sharded exchange keys (BASELINE config 4)
 $(BUILD)/gmm_kernels_shard.o: $(SRC)/gmm_kernels_shard.hip $(HDRS)

@@ -92,6 +92,12 @@ typedef struct {
  * height (tests, A/B timing; TILE32 applies only within those limits). */
 #define GMM_FLAG_SPLIT_TILE16 2u
 #define GMM_FLAG_SPLIT_TILE32 4u
+/* diagonal-maximum, batch-diagonal-maximum-float: evaluate every density in the reference's own f32
+ * operation order (GaussDiagonalMaximumFeatureScorer::distance, GDMFS.cc:144-181;
+ * BatchFloatFeatureScorer::fillScoreCacheTpl, BatchFeatureScorer.cc:187-234) on the vector ALUs: scores
+ * and best densities bit-identical to the reference's arithmetic, at a fraction of the matrix-core
+ * kernels' rate.  Dimension <= 128; other types refuse the flag. */
+#define GMM_FLAG_REFERENCE_ORDER 8u
 
 typedef struct gmm_scorer gmm_scorer;
 

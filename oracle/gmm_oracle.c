@@ -365,7 +365,12 @@ int orc_float_prepare(const orc_mixture_set* ms, float mixture_weight_scale, flo
     const uint32_t D = ms->dimension, C = ms->n_covariances;
     uint32_t       c, k, e;
     /* GaussDiagonalMaximumFeatureScorer ctor: gaussianScale_(std::sqrt(paramGaussianScale(c))) -- cc:51 */
-    float gs = (float)sqrt((double)gaussian_scale);
+    /* gaussianScale_ is a member set in the constructor and scale() squares the value it is passed, so
+     * neither sees sqrt(g) * sqrt(g) (which gcc -ffast-math would fold to g): both go through memory */
+    volatile float gsv  = (float)sqrt((double)gaussian_scale);
+    const float    gs   = gsv;
+    volatile float gs2v = gs * gs;
+    const float    gs2  = gs2v;
     memset(out, 0, sizeof(*out));
     out->dimension     = D;
     out->n_covariances = C;
@@ -381,10 +386,13 @@ int orc_float_prepare(const orc_mixture_set* ms, float mixture_weight_scale, flo
             out->isv[(size_t)c * D + k] = orc_inverse_sqrt(var[k]);
         }
         out->log_norm[c] = (float)orc_gauss_log_norm(var, D);
-        /* covarianceTable_[i].scale(gaussianScale_) */
+        /* covarianceTable_[i].scale(gaussianScale_): logNormalizationFactor_ *= factor * factor
+         * (CovarianceFeatureScorerElement.cc:45-51).  Compiled by itself, with the reference's flags, that
+         * function squares the factor first (x * (f * f)); written inline here, gcc -ffast-math would
+         * reassociate it into (x * f) * f, so the square is formed separately. */
         for (k = 0; k < D; ++k)
             out->isv[(size_t)c * D + k] = out->isv[(size_t)c * D + k] * gs;
-        out->log_norm[c] *= gs * gs;
+        out->log_norm[c] = out->log_norm[c] * gs2;
     }
     /* mixtureTable_[i] = *mixture(i); scale(mixtureWeightScale_) -- MixtureFeatureScorerElement.cc:21-33 */
     out->minus2_log_weight = (float*)malloc(sizeof(float) * out->n_entries);

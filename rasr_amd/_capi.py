@@ -17,6 +17,7 @@ GMM_OK = 0
 GMM_FLAG_NATIVE_F32 = 1  # gmm_scorer_config.flags
 GMM_FLAG_SPLIT_TILE16 = 2
 GMM_FLAG_SPLIT_TILE32 = 4
+GMM_FLAG_REFERENCE_ORDER = 8  # diagonal-maximum / batch-float in the reference's f32 operation order
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0

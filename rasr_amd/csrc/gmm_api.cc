@@ -81,6 +81,8 @@ struct gmm_scorer {
     bool              multiCov   = false;
     bool              foldNorm   = false;
     bool              split      = false;  // float types on the split-f16 kernel
+    bool              direct     = false;  // float types in the reference's operation order (scoreDirect)
+    uint32_t          directL    = 0;      // row length of the direct layout
     uint32_t          kSteps16   = 0;      // split kernel: K steps (32 wide for 16-row tiles, 16 wide for 32-row)
     uint32_t          splitRows  = 16;     // split kernel tile height
     uint32_t          tileBits   = 1;
@@ -105,6 +107,10 @@ struct gmm_scorer {
     uint32_t* dMixTileOff = nullptr;
     float*    dIsv       = nullptr;
     float*    dCentre    = nullptr;  // float types: centre of the expanded quadratic form [D]
+    float*    dDirMean   = nullptr;  // reference-order layout (PreparedDirect)
+    float*    dDirConst  = nullptr;
+    float*    dDirLogNorm = nullptr;
+    uint32_t* dDirCov    = nullptr;
     // device frame staging
     int8_t*  dFrameQ  = nullptr;
     int32_t* dFrameSS = nullptr;
@@ -136,7 +142,8 @@ struct gmm_scorer {
     ~gmm_scorer() {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
                         dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
-                        dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu, dCentre};
+                        dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu, dCentre,
+                        dDirMean, dDirConst, dDirLogNorm, dDirCov};
         for (void* p : ptrs)
             if (p)
                 (void)hipFree(p);
@@ -165,6 +172,8 @@ namespace {
 uint32_t framesPerBlock(const gmm_scorer* s) {
     if (s->quantized)
         return s->presel ? kI8PreselFramesPerBlock : kI8FramesPerBlock;
+    if (s->direct)
+        return kDirectFramesPerBlock;
     return s->split ? kSplitFramesPerBlock : kF32FramesPerBlock;
 }
 
@@ -299,6 +308,33 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         GMM_HIP_CHECK(launchScoreI8(a, s->kSteps, s->multiCov, stream));
+        GMM_HIP_CHECK(span.end());
+    }
+    else if (s->direct) {
+        DirectArgs a{};
+        a.mean        = s->dDirMean;
+        a.isv         = s->dIsv;
+        a.entryCov    = s->dDirCov;
+        a.constant    = s->dDirConst;
+        a.logNorm     = s->dDirLogNorm;
+        a.mixOff      = s->dMixTileOff;
+        a.chunkMixOff = ct->dMixOff;
+        a.frames      = frames;
+        a.scores      = scores;
+        a.best        = s->flavor == Flavor::DiagonalMaximum ? best : nullptr;
+        a.nFrames     = nFrames;
+        a.frameStride = frameStride;
+        a.scoreStride = scoreStride;
+        a.nChunks     = ct->nChunks;
+        a.nFrameTiles = nFrameTiles;
+        a.D           = s->D;
+        a.Dp          = s->directL;
+        a.batch       = s->flavor == Flavor::BatchFloat ? 1 : 0;
+        a.multiCov    = s->C > 1 ? 1 : 0;
+        a.outScale    = s->cfg.score_scale;
+        TimedSpan span(s, stream);
+        GMM_HIP_CHECK(span.begin());
+        GMM_HIP_CHECK(launchScoreDirect(a, stream));
         GMM_HIP_CHECK(span.end());
     }
     else if (s->split) {
@@ -617,6 +653,10 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
                                          "the reference's fixed 48-byte loads are undefined for smaller dimensions; "
                                          "use batch-diagonal-maximum-int");
     const bool presel = type == GMM_BATCH_PRESELECTION_FLOAT || type == GMM_BATCH_PRESELECTION_INT;
+    const bool direct = (cfg.flags & GMM_FLAG_REFERENCE_ORDER) != 0;
+    if (direct && type != GMM_DIAGONAL_MAXIMUM && type != GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT)
+        return fail(GMM_ERR_UNSUPPORTED, "the reference-order flag applies to diagonal-maximum and "
+                                         "batch-diagonal-maximum-float only");
     if (presel && (cfg.clusters == 0 || cfg.clusters > 256))
         return fail(GMM_ERR_INVALID_ARGUMENT, "clusters must be in [1, 256]");
     if (presel && (cfg.flags & (GMM_FLAG_NATIVE_F32 | GMM_FLAG_SPLIT_TILE32)))
@@ -681,6 +721,23 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
         // BatchPreselectionIntFeatureScorer::init: clustering_->build(means_) over the u8 means
         if (presel && (rc = setupPreselection(s.get(), *ms, p.preparedMean.data(), p.paddedDimension,
                                               p.tiling.rowEntry, nullptr)) != GMM_OK)
+            return rc;
+    }
+    else if (direct) {
+        PreparedDirect p;
+        std::string    err = prepareDirect(*ms, flavor, cfg.mixture_weight_scale, cfg.gaussian_scale, shard,
+                                           directBlocks(ms->dimension, flavor == Flavor::BatchFloat), p);
+        if (!err.empty())
+            return fail(GMM_ERR_INVALID_ARGUMENT, err);
+        s->direct     = true;
+        s->directL    = p.L;
+        s->nMix       = p.nMixtures;
+        s->multiCov   = s->C > 1;
+        s->nTiles     = p.nEntries;  // chunks are cut by entries (chunkTableFor)
+        s->mixTileOff = p.mixOff;
+        if ((rc = upload(&s->dDirMean, p.mean)) || (rc = upload(&s->dIsv, p.isv)) || (rc = upload(&s->dDirCov, p.entryCov)) ||
+            (rc = upload(&s->dDirConst, p.constant)) || (rc = upload(&s->dDirLogNorm, p.logNorm)) ||
+            (rc = upload(&s->dMixTileOff, s->mixTileOff)))
             return rc;
     }
     else {
@@ -899,7 +956,7 @@ int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLau
     if (nLaunches)
         *nLaunches = s->presel ? 3 : 2;
     if (name)
-        *name = s->quantized ? "scoreI8" : (s->split ? (s->flavor == Flavor::DiagonalSum ? "scoreSplitSum"
+        *name = s->quantized ? "scoreI8" : s->direct ? "scoreDirect" : (s->split ? (s->flavor == Flavor::DiagonalSum ? "scoreSplitSum"
                                                                          : (s->splitRows == 32 ? "scoreSplit32" : "scoreSplit"))
                                                        : "scoreF32");
     return GMM_OK;

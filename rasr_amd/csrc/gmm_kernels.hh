@@ -124,6 +124,30 @@ hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps, 
 hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps, hipStream_t stream);  // diagonal-sum, 16-row tiles
 constexpr uint32_t kSplit32MaxKSteps = 10;  // 32-row split kernel instantiated for K/16 <= 10 (D <= 51)
 hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
+
+// reference-order float scorers (GMM_FLAG_REFERENCE_ORDER, gmm_kernels_direct.hip): one frame per lane, the
+// reference's own f32 operation order per density, densities streamed through the scalar cache
+constexpr uint32_t kDirectFramesPerBlock = 256;
+struct DirectArgs {
+    const float*    mean;         // [entries][Dp]: diagonal-maximum the means, batch-float mean * isv (f32)
+    const float*    isv;          // [C][Dp]: 1/sqrt(var) (diagonal-maximum: times sqrt(gaussian-scale))
+    const uint32_t* entryCov;     // [entries]
+    const float*    constant;     // [entries]: minus2LogWeights (diagonal-maximum) / constants_ (batch-float)
+    const float*    logNorm;      // [C] (diagonal-maximum)
+    const uint32_t* mixOff;       // [nMixtures+1] entry offsets (shard-relative)
+    const uint32_t* chunkMixOff;  // [nChunks+1]
+    const float*    frames;
+    float*          scores;
+    uint32_t*       best;
+    uint32_t        nFrames, frameStride, scoreStride;
+    uint32_t        nChunks, nFrameTiles;
+    uint32_t        D, Dp;        // Dp: row length L = 4 NB + 4 floats (directBlocks)
+    int             batch;        // 0 diagonal-maximum, 1 batch-diagonal-maximum-float
+    int             multiCov;     // several covariances (isv row per density)
+    float           outScale;
+};
+hipError_t launchScoreDirect(const DirectArgs& a, hipStream_t stream);
+uint32_t   directBlocks(uint32_t D, bool batch);  // 4-dimension blocks of the row layout, 0 = unsupported
 constexpr uint32_t kI8PreselNF           = 4;  // preselection-batch-int: 64 frames per wave (one mask word)
 constexpr uint32_t kI8PreselFramesPerBlock = kWavesPerBlock * kI8PreselNF * 16;
 

@@ -617,4 +617,70 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
     return "";
 }
 
+// ---------------------------------------------------------------------------
+// reference-order float scorers
+// ---------------------------------------------------------------------------
+
+std::string prepareDirect(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
+                          ShardRange shard, uint32_t nb, PreparedDirect& out) {
+    std::string err = validate(ms);
+    if (!err.empty())
+        return err;
+    shard = normalizeShard(ms, shard);
+    if (shard.begin > shard.end || shard.end > ms.n_mixtures)
+        return "invalid mixture shard";
+    const uint32_t D = ms.dimension, C = ms.n_covariances;
+    const bool     batch = flavor == Flavor::BatchFloat;
+    if (batch && C != 1)
+        return "feature scorer supports only globally pooled covariance";  // BatchFeatureScorer.cc:146-148
+    if (D > 128 || nb == 0 || (batch ? 4 * nb < (D + 7) / 8 * 8 : nb < D / 4))
+        return "reference-order scorer supports dimension <= 128";
+    out     = PreparedDirect();
+    out.nb  = nb;
+    out.L   = 4 * nb + 4;
+    const uint32_t L = out.L, nfb = D / 4;
+    // slot of dimension k in the row layout (gmm_kernels_direct.hip)
+    const auto slot = [&](uint32_t k) { return batch || k < 4 * nfb ? k : 4 * nb + (k - 4 * nfb); };
+
+    // diagonal-maximum: GaussDiagonalMaximumFeatureScorer::init (GDMFS.cc:64-86): isv and logNorm scaled by
+    // gaussianScale_ = sqrt(gaussian-scale), minus2LogWeights scaled by mixture-weight-scale; batch-float:
+    // BatchFloatFeatureScorer::init (BatchFeatureScorer.cc:145-175), unscaled
+    const float gs = batch ? 1.0f : static_cast<float>(std::sqrt(static_cast<double>(gaussianScale)));
+    out.isv.assign(static_cast<size_t>(C) * L, 0.0f);
+    out.logNorm.resize(C);
+    for (uint32_t c = 0; c < C; ++c) {
+        const float* var = ms.variances + static_cast<size_t>(c) * D;
+        for (uint32_t k = 0; k < D; ++k) {
+            const float iv = refInverseSqrt(var[k]);
+            out.isv[static_cast<size_t>(c) * L + slot(k)] = batch ? iv : iv * gs;
+        }
+        const float ln = static_cast<float>(refGaussLogNorm(var, D));
+        out.logNorm[c] = batch ? ln : ln * (gs * gs);
+    }
+    const uint32_t eb = ms.mixture_offsets[shard.begin], ee = ms.mixture_offsets[shard.end];
+    out.nMixtures = shard.end - shard.begin;
+    out.nEntries  = ee - eb;
+    out.mixOff.resize(out.nMixtures + 1);
+    for (uint32_t m = 0; m <= out.nMixtures; ++m)
+        out.mixOff[m] = ms.mixture_offsets[shard.begin + m] - eb;
+    out.mean.assign(static_cast<size_t>(out.nEntries) * L, 0.0f);
+    out.entryCov.resize(out.nEntries);
+    out.constant.resize(out.nEntries);
+    for (uint32_t e = eb; e < ee; ++e) {
+        const uint32_t dns  = ms.mixture_densities[e];
+        const uint32_t cov  = ms.density_covariance[dns];
+        const float*   mean = ms.means + static_cast<size_t>(ms.density_mean[dns]) * D;
+        float*         row  = out.mean.data() + static_cast<size_t>(e - eb) * L;
+        for (uint32_t k = 0; k < D; ++k)  // batch: means_ = mean * variance_ (std::multiplies<float>, cc:171)
+            row[slot(k)] = batch ? mean[k] * out.isv[k] : mean[k];
+        out.entryCov[e - eb] = cov;
+        const double lw      = ms.mixture_log_weights[e];
+        // MixtureFeatureScorerElement.cc:26,30-33: (f32)(-2 log w) * scale; BatchFeatureScorer.cc:173:
+        // constants_ = logNormFactor - 2 * logWeight
+        out.constant[e - eb] = batch ? static_cast<float>(static_cast<double>(out.logNorm[0]) - 2 * lw)
+                                     : static_cast<float>(-2 * lw) * mixtureWeightScale;
+    }
+    return "";
+}
+
 }  // namespace rasr_gmm

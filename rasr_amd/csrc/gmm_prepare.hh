@@ -115,6 +115,20 @@ struct ShardRange {
     uint32_t begin = 0, end = 0;
 };
 
+// Reference-order float scorers (GMM_FLAG_REFERENCE_ORDER, gmm_kernels_direct.hip): rows of L = 4 nb + 4
+// floats per mixture entry (diagonal-maximum: the D / 4 whole 4-dimension blocks, zeros, the D % 4
+// remaining dimensions in the last 4 slots; batch-float: mean * isv, zeros), the covariances' isv rows in
+// the same layout, the per-entry constants and covariance, CSR entry offsets of the shard's mixtures.
+struct PreparedDirect {
+    uint32_t              nb = 0, L = 0, nMixtures = 0, nEntries = 0;
+    std::vector<float>    mean;       // [nEntries][L]
+    std::vector<float>    isv;        // [C][L]
+    std::vector<uint32_t> entryCov;   // [nEntries]
+    std::vector<float>    constant;   // [nEntries] minus2LogWeights / batch constants_
+    std::vector<float>    logNorm;    // [C]
+    std::vector<uint32_t> mixOff;     // [nMixtures + 1]
+};
+
 // Returns empty string on success, else an error message.
 std::string validate(const gmm_mixture_set& ms);
 std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out);
@@ -122,5 +136,8 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
 // 3*dimension+7 <= 256, row constants below 2^30); out.split says whether it did.
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
                          ShardRange shard, PreparedFloat& out, bool wantSplit = false, uint32_t splitRowsWanted = 0);
+// nb: 4-dimension blocks of the kernel instantiation (directBlocks)
+std::string prepareDirect(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,
+                          ShardRange shard, uint32_t nb, PreparedDirect& out);
 
 }  // namespace rasr_gmm

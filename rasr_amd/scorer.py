@@ -32,7 +32,8 @@ class Scorer:
                  device: int = 0, mixture_weight_scale: float = 1.0, gaussian_scale: float = 1.0,
                  score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None, native_f32: bool = False,
                  split_tile16: bool = False, split_tile32: bool = False, clusters: int = 256,
-                 select_clusters: int = 32, clustering_iterations: int = 5, backoff_score: float = 40000.0):
+                 select_clusters: int = 32, clustering_iterations: int = 5, backoff_score: float = 40000.0,
+                 reference_order: bool = False):
         self._lib = _capi.load_library()
         self.mixture_set = mixture_set
         self.type = _type_id(scorer_type)
@@ -47,6 +48,8 @@ class Scorer:
             cfg.flags |= _capi.GMM_FLAG_SPLIT_TILE16
         if split_tile32:  # split-f16 kernel: force 32-density tiles (mixtures <= 512 densities, D <= 51)
             cfg.flags |= _capi.GMM_FLAG_SPLIT_TILE32
+        if reference_order:  # float types: the reference's own f32 operation order (bit-identical, VALU rate)
+            cfg.flags |= _capi.GMM_FLAG_REFERENCE_ORDER
         # density preselection ("density-clustering" parameters, preselection-batch-* types)
         cfg.clusters = int(clusters)
         cfg.select_clusters = int(select_clusters)
