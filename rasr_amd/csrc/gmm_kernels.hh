@@ -148,6 +148,9 @@ struct DirectArgs {
 };
 hipError_t launchScoreDirect(const DirectArgs& a, hipStream_t stream);
 uint32_t   directBlocks(uint32_t D, bool batch);  // 4-dimension blocks of the row layout, 0 = unsupported
+// quantized LDS kernel: the never-winning stand-in tile after the segment ring (operands, row constants,
+// PRESEL cluster offsets)
+constexpr uint32_t kI8DummyTileBytes(int ks, bool presel) { return static_cast<uint32_t>(ks) * 1024u + 64u + (presel ? 32u : 0u); }
 constexpr uint32_t kI8PreselNF           = 4;  // preselection-batch-int: 64 frames per wave (one mask word)
 constexpr uint32_t kI8PreselFramesPerBlock = kWavesPerBlock * kI8PreselNF * 16;
 

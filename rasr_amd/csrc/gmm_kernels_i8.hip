@@ -379,8 +379,13 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
     constexpr int      kPieces   = kSegTiles * KS / 4;          // 1 KiB pieces per wave per segment
     constexpr int      kIssued   = kPieces + 1 + (PRESEL ? 1 : 0);  // vector memory ops per wave per segment
     static_assert(kSegTiles * KS % 4 == 0, "segment pieces must split evenly over 4 waves");
+    // after the ring: the stand-in second tile of a step that has one tile left (odd tile count, segment
+    // end): zero operands (dot = 0), rows that never win, cluster offsets 0.  Every step is then a pair
+    // step: one loop body, whose running minima stay in their registers (a second, single-tile body made
+    // the compiler copy all NF*4 minima back at every step that did not end a mixture)
+    constexpr uint32_t kDummyBytes = kI8DummyTileBytes(KS, PRESEL);
     // one __shared__ array only (a second one can make hipcc drain vmcnt before LDS reads)
-    __shared__ __attribute__((aligned(16))) int8_t ldsStatic[PRESEL ? 16 : 2 * kSegBytes];
+    __shared__ __attribute__((aligned(16))) int8_t ldsStatic[PRESEL ? 16 : 2 * kSegBytes + kDummyBytes];
     int8_t* const lds = PRESEL ? i8DynLds : ldsStatic;
 
     const int lane = threadIdx.x & 63;
@@ -418,6 +423,14 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
                                                  base + kSegP + wave * (kSegTiles * 8), 16, 0, 0);
         }
     };
+    {
+        int8_t* const dummy = lds + 2 * kSegBytes;
+        // non-PRESEL rows compare signed (INT_MAX never wins), PRESEL rows unsigned (biased: all ones)
+        const uint32_t never = PRESEL ? 0xffffffffu : 0x7fffffffu;
+        for (uint32_t i = threadIdx.x; i < kDummyBytes / 4; i += 256u)
+            reinterpret_cast<uint32_t*>(dummy)[i] = (i >= kTileA / 4 && i < kTileA / 4 + 16) ? never : 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before use by the first segment's barrier
+    }
     if (nSeg > 0)
         issueSeg(0);
     if (nSeg > 1)
@@ -442,16 +455,18 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
     if constexpr (PRESEL) {
         const uint32_t words = a.nClusters * 16u;
         const i32x4*   src   = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
-        i32x4*         dst   = reinterpret_cast<i32x4*>(lds + 2 * kSegBytes + static_cast<uint32_t>(wave) * words * 4u);
+        i32x4*         dst   = reinterpret_cast<i32x4*>(lds + 2 * kSegBytes + kDummyBytes + static_cast<uint32_t>(wave) * words * 4u);
         for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u)
             dst[i] = src[i];
-        laneSel = 2 * kSegBytes + (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
+        laneSel = 2 * kSegBytes + kDummyBytes + (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
     }
-    // a tile's row constants (the host biases them by 2^31 for PRESEL) and mask words of this lane's 4 rows
-    const auto tileRows = [&](const int8_t* base, uint32_t lt, i32x4& P, uint32_t(&T)[4]) {
-        P = *reinterpret_cast<const i32x4*>(base + kSegA + lt * 64 + g * 16);
+    // a tile's row constants (the host biases them by 2^31 for PRESEL) and mask words of this lane's 4 rows,
+    // from the tile's 64-byte row-constant block pRow and 32-byte cluster-offset block cRow
+    const auto tileRows = [&](const int8_t* pRow, const int8_t* cRow, i32x4& P, uint32_t(&T)[4]) {
+        P = *reinterpret_cast<const i32x4*>(pRow + g * 16);
+        (void)cRow;
         if constexpr (PRESEL) {
-            const uint2 cw = *reinterpret_cast<const uint2*>(base + kSegP + lt * 32 + g * 8);
+            const uint2 cw = *reinterpret_cast<const uint2*>(cRow + g * 8);
             const int8_t* tb = lds + laneSel;
             T[0] = *reinterpret_cast<const uint32_t*>(tb + (cw.x & 0xffffu));
             T[1] = *reinterpret_cast<const uint32_t*>(tb + (cw.x >> 16));
@@ -527,67 +542,51 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
         uint32_t       t      = segT0;
         while (t < segEnd) {
             const uint32_t lt = (GMM_I8_DIAG & 16) ? 0u : t - segT0;
-            if (t + 1 < segEnd && t + 1 < tEnd) {
-                // two tiles of the same mixture: 2 NF independent MFMAs, one v_min3 per candidate pair
-                i32x4 A0[KS], A1[KS];
+            // two tiles of the same mixture, or the last one beside the never-winning stand-in:
+            // 2 NF independent MFMAs, one v_min3 per candidate pair
+            const bool          two   = t + 1 < segEnd && t + 1 < tEnd;  // uniform
+            const int8_t* const dummy = lds + 2 * kSegBytes;
+            const int8_t* const a0    = base + lt * kTileA;
+            const int8_t* const a1    = two ? a0 + kTileA : dummy;
+            const int8_t* const p0    = base + kSegA + lt * 64;
+            const int8_t* const p1    = two ? p0 + 64 : dummy + kTileA;
+            const int8_t* const c0    = base + kSegP + lt * 32;
+            const int8_t* const c1    = two ? c0 + 32 : dummy + kTileA + 64;
+            i32x4               A0[KS], A1[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                A0[ks] = *reinterpret_cast<const i32x4*>(a0 + ks * 1024 + lane * 16);
+                A1[ks] = *reinterpret_cast<const i32x4*>(a1 + ks * 1024 + lane * 16);
+            }
+            i32x4    P0, P1;
+            uint32_t T0w[4] = {}, T1w[4] = {};
+            tileRows(p0, c0, P0, T0w);
+            tileRows(p1, c1, P1, T1w);
+            i32x4 accA[NF], accB[NF];
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb) {
+                accA[cb] = i32x4{0, 0, 0, 0};
+                accB[cb] = i32x4{0, 0, 0, 0};
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks) {
-                    A0[ks] = *reinterpret_cast<const i32x4*>(base + lt * kTileA + ks * 1024 + lane * 16);
-                    A1[ks] = *reinterpret_cast<const i32x4*>(base + (lt + 1) * kTileA + ks * 1024 + lane * 16);
+                    accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
+                    accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[ks], B[cb][ks], accB[cb], 0, 0, 0);
                 }
-                i32x4    P0, P1;
-                uint32_t T0w[4] = {}, T1w[4] = {};
-                tileRows(base, lt, P0, T0w);
-                tileRows(base, lt + 1, P1, T1w);
-                i32x4 accA[NF], accB[NF];
+            }
 #pragma unroll
-                for (int cb = 0; cb < NF; ++cb) {
-                    accA[cb] = i32x4{0, 0, 0, 0};
-                    accB[cb] = i32x4{0, 0, 0, 0};
+            for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) {
-                        accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
-                        accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[ks], B[cb][ks], accB[cb], 0, 0, 0);
-                    }
-                }
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        best[cb][r] = min2(best[cb][r], min2(cand(accA[cb][r], P0[r], T0w[r], cb),
-                                                             cand(accB[cb][r], P1[r], T1w[r], cb)));
+                for (int r = 0; r < 4; ++r)
+                    best[cb][r] = min2(best[cb][r], min2(cand(accA[cb][r], P0[r], T0w[r], cb),
+                                                         cand(accB[cb][r], P1[r], T1w[r], cb)));
 #if GMM_I8_INTERLEAVE
 #pragma unroll
-                for (int i = 0; i < 2 * NF * KS; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, GMM_I8_INTERLEAVE, 0);  // VALU
-                }
+            for (int i = 0; i < 2 * NF * KS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, GMM_I8_INTERLEAVE, 0);  // VALU
+            }
 #endif
-                t += 2;
-            }
-            else {
-                i32x4 A0[KS];
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks)
-                    A0[ks] = *reinterpret_cast<const i32x4*>(base + lt * kTileA + ks * 1024 + lane * 16);
-                i32x4    P0;
-                uint32_t T0w[4] = {};
-                tileRows(base, lt, P0, T0w);
-                i32x4 accA[NF];
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb) {
-                    accA[cb] = i32x4{0, 0, 0, 0};
-#pragma unroll
-                    for (int ks = 0; ks < KS; ++ks)
-                        accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
-                }
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        best[cb][r] = min2(best[cb][r], cand(accA[cb][r], P0[r], T0w[r], cb));
-                t += 1;
-            }
+            t += two ? 2u : 1u;
             // mixture(s) ending here (further ones without tiles end at the same point)
             while (t == tEnd && m < m1) {
                 emit(m);
@@ -622,7 +621,7 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
     if constexpr (!MULTI) {
         if (a.presel) {  // preselection-batch-int: NF 4, 4-tile segments (ring + 4 mask tables < 80 KiB)
             constexpr int      kSeg  = 4;
-            constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 32));
+            constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 32)) + kI8DummyTileBytes(KS, true);
             const uint32_t     lds   = kRing + 4u * a.nClusters * 64u;
             static bool        attr  = false;
             if (!attr) {
