@@ -91,8 +91,12 @@ __global__ __launch_bounds__(256) void prepareFramesI8(const float* __restrict__
 // quantized scorer
 // ---------------------------------------------------------------------------
 // Per-mixture end: 4 rows in-lane, reduce-scatter over the 4 lane groups, finalize and store the
-// scores (and best densities) of the wave's NF*16 frames for mixture m.
-template <int NF>
+// scores (and best densities) of the wave's NF*16 frames for mixture m.  MAYBE_NONE: the minimum may
+// still be INT_MAX (a mixture without densities; preselection: none selected).  A mixture with tiles
+// never reaches INT_MAX otherwise (the host bounds every real row's packed value below 2^31 - 2^(ib+1),
+// gmm_prepare.cc), so the scorer's per-mixture emit skips those selects (v_cndmask issues at a
+// quarter of the rate of the other VALU ops).
+template <int NF, bool MAYBE_NONE = true>
 __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict__ scores, uint32_t* __restrict__ bestOut,
                                               const int (&best)[NF][4], uint32_t m, uint32_t frame0, int lane, int g,
                                               int ib, const int (&ssOut)[NF / 4]) {
@@ -148,7 +152,7 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
 #endif
         const int packed = res[i];
         // mixture without densities: minScore stays Core::Type<int>::max
-        const bool     none = packed == INT_MAX;
+        const bool     none = MAYBE_NONE && packed == INT_MAX;
         const int      q    = none ? INT_MAX : (packed >> ib) + ssOut[i];
         const uint32_t dns  = none ? 0xffffffffu : static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
         float score;
@@ -172,8 +176,9 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
         }
         else  // BatchFeatureScorer.cc:468: (f32)best / scale_
             score = __fdiv_rn(static_cast<float>(q), a.batchScale);
-        if (a.outScale != 1.0f)
-            score = __fmul_rn(a.outScale, score);  // ScaledContextScorer::score, ScaledFeatureScorer.hh:62-64
+        // ScaledContextScorer::score (ScaledFeatureScorer.hh:62-64); a finite score times 1.0f is itself,
+        // so the multiply is unconditional (a select on the uniform test costs more than the multiply)
+        score = __fmul_rn(a.outScale, score);
 #if GMM_I8_BUFSTORE
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, f * 4u, 0, 0);
         if (bestOut)
@@ -503,7 +508,9 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
             for (int r = 0; r < 4; ++r)
                 best[cb][r] = PRESEL ? -1 : INT_MAX;  // PRESEL: 0xffffffff = biased INT_MAX
     };
-    const auto emit = [&](uint32_t mm) {
+    // hot: the end of a mixture with tiles (its minimum is a real row: no INT_MAX case, unless PRESEL)
+    const auto emit = [&](uint32_t mm, auto hot) {
+        constexpr bool kMaybeNone = PRESEL || !decltype(hot)::value;
         if constexpr (PRESEL) {
             int unb[NF][4];
 #pragma unroll
@@ -511,19 +518,21 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     unb[cb][r] = static_cast<int>(static_cast<uint32_t>(best[cb][r]) ^ 0x80000000u);
-            emitMixtureI8<NF>(a, scores, bestOut, unb, mm, frame0, lane, g, ib, ssOut);
+            emitMixtureI8<NF, kMaybeNone>(a, scores, bestOut, unb, mm, frame0, lane, g, ib, ssOut);
         }
         else {
             if (!(GMM_I8_DIAG & 4) || mm + 1 == m1)
-                emitMixtureI8<NF>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
+                emitMixtureI8<NF, kMaybeNone>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
         }
     };
+    const std::true_type  kHot{};
+    const std::false_type kEmpty{};
     resetBest();
     uint32_t m    = m0;
     uint32_t tEnd = mixTileOff[m0 + 1];
     // mixtures without tiles at the start of the chunk
     while (m < m1 && tEnd == T0) {
-        emit(m);
+        emit(m, kEmpty);
         ++m;
         tEnd = m < m1 ? mixTileOff[m + 1] : T1;
     }
@@ -587,12 +596,17 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
             }
 #endif
             t += two ? 2u : 1u;
-            // mixture(s) ending here (further ones without tiles end at the same point)
-            while (t == tEnd && m < m1) {
-                emit(m);
+            // the mixture ending here, and further ones without tiles ending at the same point (rare)
+            if (t == tEnd && m < m1) {
+                emit(m, kHot);
                 resetBest();
                 ++m;
                 tEnd = m < m1 ? mixTileOff[m + 1] : T1;
+                while (t == tEnd && m < m1) {
+                    emit(m, kEmpty);
+                    ++m;
+                    tEnd = m < m1 ? mixTileOff[m + 1] : T1;
+                }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
