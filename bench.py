@@ -72,7 +72,7 @@ MODES = {
 }
 FRAMES_PER_LAUNCH = 32768  # frames per scorer call (the scorer's max_frames)
 # scorer calls per step: about 50-60 ms of GPU work per step at the measured rates, so 20 steps >= 1 s
-DEFAULT_LAUNCHES = {"fp32": 12, "simd": 24, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
+DEFAULT_LAUNCHES = {"fp32": 12, "simd": 32, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
 # BASELINE config 5 network (hybrid DNN): 11 x 39 spliced MFCC input, 6 sigmoid layers of 2048, 5000 classes
 NN_DIMS = [429] + [2048] * 6 + [5000]
 
