@@ -34,6 +34,8 @@ for s in $STEPS; do
     bench_ragged) step bench_ragged 600 python bench.py --ragged --steps 20 --warmup 3 --cpu-baseline off --host-boundary off ;;
     bench_sum) step bench_sum 600 python bench.py --mode sum --steps 20 --warmup 3 --cpu-baseline off --host-boundary off --no-extra-mode ;;
     bench_nn) step bench_nn 600 python bench.py --mode nn --steps 20 --warmup 3 ;;
+    bench_presel) step bench_presel_int 600 python bench.py --mode presel-int --steps 10 --warmup 2 --cpu-baseline off --host-boundary off --no-extra-mode &&
+                  step bench_presel_float 600 python bench.py --mode presel-float --steps 10 --warmup 2 --cpu-baseline off --host-boundary off --no-extra-mode ;;
     pytest_new) step pytest_new 1200 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $PYTEST_ARGS ;;
   esac
 done
