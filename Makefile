@@ -11,8 +11,9 @@ I8FLAGS   = -mllvm -amdgpu-mfma-vgpr-form
 # float kernels: default AGPR accumulators (measured faster for the f32 MFMA chains) and one
 # tile per loop step (GMM_F32_PAIR=0), see DESIGN.md "Measurements"
 F32FLAGS  = -DGMM_F32_PAIR=0
-# split-f16 float kernel
-SPLITFLAGS = -mllvm -amdgpu-mfma-vgpr-form
+# split-f16 float kernel; no SLP packing: the diagonal-sum epilogue's adds were packed into v_pk_add_f32 /
+# v_pk_mul_f32, which issue slower than two scalar ops beside the MFMAs (A/B: -1.0 %; no packed ops elsewhere)
+SPLITFLAGS = -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize
 HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc

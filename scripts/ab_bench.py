@@ -3,7 +3,7 @@
 
 Each variant runs in its own subprocess (RASR_GMM_LIB=<so>); rounds are interleaved
 (v1 v2 ... v1 v2 ...) and the median / min kernel time per variant is reported.
-usage: ab_bench.py --mode fp32|simd --rounds 3 lib1.so lib2.so[:split16|:split32] ...
+usage: ab_bench.py --mode fp32|simd|sum --rounds 3 lib1.so lib2.so[:split16|:split32] ...
 (":split16" / ":split32" run that library with GMM_FLAG_SPLIT_TILE16 / _TILE32)
 """
 import argparse
@@ -20,7 +20,7 @@ import os, sys, json, time
 sys.path.insert(0, os.environ["ROOT"])
 import torch, rasr_amd as ra
 mode = os.environ["MODE"]; F = int(os.environ["FRAMES"])
-kind = "diagonal-maximum" if mode == "fp32" else "SIMD-diagonal-maximum"
+kind = {"fp32": "diagonal-maximum", "simd": "SIMD-diagonal-maximum", "sum": "diagonal-sum"}[mode]
 D = int(os.environ.get("DIM", "39"))
 ms = ra.synthetic_mixture_set(5000, 160, D, seed=2024)
 sc = ra.Scorer(ms, kind, max_frames=F, split_tile16=os.environ.get("SPLIT") == "16",
