@@ -14,6 +14,12 @@ namespace dev {
 typedef int   i32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef GMM_STORE_CPOL
+// cache policy of the score-table stores: 2 = non-temporal (nt).  The table is written once and never
+// re-read by the kernel; streaming it leaves the L2 to the model tiles every frame tile of a chunk
+// re-reads (A/B, profiles/r02/ab/ab_store_nt.txt: -1.4 % fp32, -0.35 % SIMD)
+#define GMM_STORE_CPOL 2
+#endif
 #ifndef GMM_PERMLANE
 #define GMM_PERMLANE 1  // quantized kernel: reduce-scatter by v_permlane{32,16}_swap (else ds_bpermute)
 #endif

@@ -180,9 +180,9 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
         // so the multiply is unconditional (a select on the uniform test costs more than the multiply)
         score = __fmul_rn(a.outScale, score);
 #if GMM_I8_BUFSTORE
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, f * 4u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, f * 4u, 0, GMM_STORE_CPOL);
         if (bestOut)
-            __builtin_amdgcn_raw_buffer_store_b32(dns, rb, f * 4u, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(dns, rb, f * 4u, 0, GMM_STORE_CPOL);
 #else
         const size_t o = static_cast<size_t>(mo) * a.scoreStride + f;
         scores[o]      = score;

@@ -197,11 +197,11 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
     // frames >= nFrames fall outside num_records: the buffer store drops them
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
                                                      static_cast<int>(a.nFrames * 4u), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, off, 0, GMM_STORE_CPOL);
     if constexpr (BEST) {
         const auto rb = __builtin_amdgcn_make_buffer_rsrc(a.best + static_cast<size_t>(mo) * a.scoreStride, (short)0,
                                                          static_cast<int>(a.nFrames * 4u), 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, GMM_STORE_CPOL);
     }
 }
 
@@ -480,11 +480,11 @@ __device__ __forceinline__ void emitMixtureSplit32(const SplitArgs& a, const uin
     const uint32_t off = static_cast<uint32_t>(frame0 + lane) * 4u;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
                                                      static_cast<int>(a.nFrames * 4u), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, off, 0, GMM_STORE_CPOL);
     if constexpr (BEST) {
         const auto rb = __builtin_amdgcn_make_buffer_rsrc(a.best + static_cast<size_t>(mo) * a.scoreStride, (short)0,
                                                          static_cast<int>(a.nFrames * 4u), 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, GMM_STORE_CPOL);
     }
 }
 
@@ -699,11 +699,11 @@ __device__ __forceinline__ void emitMixtureSplitSum(const SplitArgs& a, const ui
     const uint32_t off = static_cast<uint32_t>(frame0 + lane) * 4u;
     const auto rs_ = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
                                                       static_cast<int>(a.nFrames * 4u), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs_, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs_, off, 0, GMM_STORE_CPOL);
     if constexpr (BEST) {
         const auto rb = __builtin_amdgcn_make_buffer_rsrc(a.best + static_cast<size_t>(mo) * a.scoreStride, (short)0,
                                                          static_cast<int>(a.nFrames * 4u), 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(idx, rb, off, 0, GMM_STORE_CPOL);
     }
 }
 
