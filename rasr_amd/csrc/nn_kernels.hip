@@ -16,6 +16,8 @@
 // one frame tile (its activations stay in that XCD's L2).
 #include "nn_kernels.hh"
 
+#include <algorithm>
+
 namespace rasr_nn {
 namespace dev {
 
@@ -632,6 +634,233 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
 #endif
 }
 
+
+// ---------------------------------------------------------------------------
+// nnGemm8pp: nnGemm8p as a persistent kernel (NN_GEMM_VARIANT 9).  With one 128 KiB workgroup per CU,
+// nnGemm8p pays every output tile's prologue (the first K-tiles from L2/HBM with nothing to overlap)
+// and epilogue (bias, activation, stores with the matrix cores idle) in the open: 4 tile rounds per
+// 2048-wide layer.  Here one workgroup per CU walks its output tiles (ids b = w, w + G, ... under the
+// same bijective XCD remap) as ONE continuous stream of K-tiles: the phase schedule, the staging two
+// K-tiles ahead and the counted waits run across tile seams unchanged, so the next tile's first K-tiles
+// land while the current tile's last ones are multiplied, and the epilogue of a tile is issued between
+// its last phase and the next tile's first.  The tile's bias (1 KiB, rows m0 .. m0+255) is staged into
+// LDS by wave 0 with the first K-tile's p1 half (double-buffered by tile parity) and is retired by that
+// step's p4 wait, before the epilogue that reads it.  The epilogue's stores are counted by vmcnt like the
+// loads: the next tile's first p4 wait also retires them.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void nnGemm8pp(NnGemmArgs a) {
+    constexpr uint32_t T = 256, BK = 64, kOp = T * BK;
+    const int          lane = threadIdx.x & 63;
+    const uint32_t     wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t     nMT = a.Mpad / T, nNT = a.Npad / T, nwg = nMT * nNT;
+    const uint32_t     G = gridDim.x, w = blockIdx.x;
+    const uint32_t     q = nwg / 8u, r = nwg % 8u;
+    const uint32_t     wr = wave >> 2, wc = wave & 3u;
+    const uint32_t     nK = a.Kpad / BK;
+    const uint32_t     nTiles = w < nwg ? (nwg - w + G - 1u) / G : 0u;
+    const uint32_t     nSteps = nTiles * nK;
+    float* const       biasLds = reinterpret_cast<float*>(nnLds + 4u * kOp);  // [2][256] after the operand buffers
+
+    // output tile of this workgroup's k-th tile (bijective XCD remap of b = w + G k, as nnGemm8p)
+    const auto tileOf = [&](uint32_t k, uint32_t& m0, uint32_t& n0) {
+        const uint32_t b = w + G * k, xcd = b & 7u;
+        const uint32_t id = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (b >> 3);
+        m0                = (id % nMT) * T;
+        n0                = (id / nMT) * T;
+    };
+    // position of a step in the stream: tile k (output tile m0, n0), K-tile u; advanced step by step
+    // (no division per stage)
+    struct Pos {
+        uint32_t k, u, m0, n0;
+    };
+    const auto advance = [&](Pos& p) {
+        if (++p.u == nK) {
+            p.u = 0;
+            ++p.k;
+            tileOf(p.k, p.m0, p.n0);
+        }
+    };
+    // stage operand op, half h of the step at p into buffer buf
+    const auto stage = [&](int op, uint32_t h, const Pos& p, uint32_t buf) {
+        const uint16_t* src  = op == 0 ? a.A : a.B;
+        const uint32_t  base = op == 0 ? p.m0 : p.n0;
+#pragma unroll
+        for (uint32_t i = 0; i < 2; ++i) {
+            const uint32_t pc  = wave * 128u + i * 64u + static_cast<uint32_t>(lane);
+            const uint32_t row = h * 128u + pc / 8u;
+            const uint32_t c   = (pc % 8u) ^ nnSwz(row);
+            __builtin_amdgcn_global_load_lds(src + static_cast<size_t>(base + row) * a.Kpad + p.u * BK + 8u * c,
+                                             nnLds + (buf * 2u + static_cast<uint32_t>(op)) * kOp + h * (kOp / 2) +
+                                                     (wave * 128u + i * 64u) * 8u,
+                                             16, 0, 0);
+        }
+    };
+    const auto frag = [&](uint32_t buf, int op, uint32_t row, uint32_t ks) {
+        const uint32_t c = ks * 4u + (static_cast<uint32_t>(lane) >> 4);
+        return *reinterpret_cast<const bf16x8*>(nnLds + (buf * 2u + static_cast<uint32_t>(op)) * kOp + row * BK +
+                                                (c ^ nnSwz(row)) * 8u);
+    };
+    const uint32_t rl = static_cast<uint32_t>(lane) & 15u;
+    typedef bf16x8 FragA[4][2];
+    typedef bf16x8 FragB[2][2];
+    const auto     readA = [&](uint32_t buf, uint32_t h, FragA& fa) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa[i][ks] = frag(buf, 0, h * 128u + wr * 64u + 16u * i + rl, ks);
+    };
+    const auto readB = [&](uint32_t buf, uint32_t h, FragB& fb) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                fb[j][ks] = frag(buf, 1, h * 128u + wc * 32u + 16u * j + rl, ks);
+    };
+    f32x4      acc[8][4];  // [4 ha + i][2 hb + j]
+    const auto zeroAcc = [&]() {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    };
+    const auto quadrant = [&](int ha, int hb, const FragA& fa, const FragB& fb) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[4 * ha + i][2 * hb + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[4 * ha + i][2 * hb + j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // the tile's bias into LDS slot k & 1 (wave 0: 64 lanes x 16 B = rows m0 .. m0 + 255)
+    const auto stageBias = [&](uint32_t k) {
+        if (wave == 0u) {
+            uint32_t m0, n0;
+            tileOf(k, m0, n0);
+            __builtin_amdgcn_global_load_lds(a.bias + m0 + 4u * static_cast<uint32_t>(lane), biasLds + (k & 1u) * 256u,
+                                             16, 0, 0);
+        }
+    };
+    // epilogue of tile k: rows m = m0 + 128 (i >> 2) + 64 wr + 16 (i & 3) + 4 (lane >> 4) + rr,
+    //                     frame n = n0 + 128 (j >> 1) + 32 wc + 16 (j & 1) + (lane & 15)
+    const auto epilogue = [&](uint32_t k) {
+        uint32_t m0, n0;
+        tileOf(k, m0, n0);
+        const uint32_t g = static_cast<uint32_t>(lane) >> 4, col = rl;
+        const float*   bl = biasLds + (k & 1u) * 256u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t mr = 128u * (i >> 2) + wr * 64u + 16u * (i & 3) + 4u * g;
+            const uint32_t mb = m0 + mr;
+            const f32x4    bs = *reinterpret_cast<const f32x4*>(bl + mr);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t n = n0 + 128u * (j >> 1) + wc * 32u + 16u * (j & 1) + col;
+                if (a.top) {
+                    if (n < a.nFrames)
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr)
+                            if (mb + rr < a.M)
+                                a.scores[static_cast<size_t>(mb + rr) * a.scoreStride + n] = -(acc[i][j][rr] + bs[rr]);
+                }
+                else {
+                    u16x4 v;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        v[rr] = toBf16(activate(acc[i][j][rr] + bs[rr], a.act, a.gamma));
+                    *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
+                }
+            }
+        }
+    };
+    if (nSteps == 0)
+        return;  // uniform over the workgroup, before any barrier
+
+    // prologue: step 0 whole, A0 / B0 of step 1, the first tile's bias; step 0 retired
+    Pos p0{0, 0, 0, 0};
+    tileOf(0, p0.m0, p0.n0);
+    Pos p1 = p0, p2;
+    advance(p1);
+    p2 = p1;
+    advance(p2);
+    stageBias(0);
+    stage(0, 0, p0, 0);
+    stage(0, 1, p0, 0);
+    stage(1, 0, p0, 0);
+    stage(1, 1, p0, 0);
+    if (nSteps > 1) {
+        stage(0, 0, p1, 1);
+        stage(1, 0, p1, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (NN8_STAGGER && wr == 1)
+        __builtin_amdgcn_s_barrier();  // the stagger
+
+    zeroAcc();
+    FragA    fa;
+    FragB    fb0, fb1;
+    uint32_t u = 0, k = 0;  // K-tile and tile of step v; p1, p2: steps v + 1, v + 2
+    for (uint32_t v = 0; v < nSteps; ++v) {
+        const uint32_t buf = v & 1u;
+        const bool     n1 = v + 1 < nSteps, n2 = v + 2 < nSteps;
+        // p1 (a tile's first step also stages its bias: retired by this step's p4 wait)
+        readA(buf, 0, fa);
+        readB(buf, 0, fb0);
+        if (u == 0u && v > 0u)
+            stageBias(k);
+        if (n1)
+            stage(1, 1, p1, buf ^ 1u);
+        __builtin_amdgcn_s_barrier();
+        quadrant(0, 0, fa, fb0);
+        __builtin_amdgcn_s_barrier();
+        // p2
+        readB(buf, 1, fb1);
+        if (n1)
+            stage(0, 1, p1, buf ^ 1u);
+        __builtin_amdgcn_s_barrier();
+        quadrant(0, 1, fa, fb1);
+        __builtin_amdgcn_s_barrier();
+        // p3
+        readA(buf, 1, fa);
+        if (n2)
+            stage(0, 0, p2, buf);
+        __builtin_amdgcn_s_barrier();
+        quadrant(1, 1, fa, fb1);
+        __builtin_amdgcn_s_barrier();
+        // p4
+        if (n2) {
+            stage(1, 0, p2, buf);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
+        else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        quadrant(1, 0, fa, fb0);
+        __builtin_amdgcn_s_barrier();
+        if (++u == nK) {  // uniform: the tile's last K-tile
+            epilogue(k);
+            zeroAcc();
+            u = 0;
+            ++k;
+        }
+        p1 = p2;
+        advance(p2);
+    }
+    if (NN8_STAGGER && wr == 0)
+        __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+}
+
 }  // namespace dev
 
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
@@ -651,8 +880,10 @@ hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream) {
     if (nwg == 0)
         return hipSuccess;
     if constexpr (kNnTileM == 256) {
-        constexpr uint32_t kLds = 2u * 2u * 256u * 64u * 2u;  // 128 KiB
-#if NN_GEMM_VARIANT == 8
+        constexpr uint32_t kLds = 2u * 2u * 256u * 64u * 2u + (NN_GEMM_VARIANT == 9 ? 2048u : 0u);  // 128 KiB (+ bias)
+#if NN_GEMM_VARIANT == 9
+        const auto kernel = dev::nnGemm8pp;
+#elif NN_GEMM_VARIANT == 8
         const auto kernel = dev::nnGemm8p;
 #else
         const auto kernel = dev::nnGemm256;
@@ -665,7 +896,20 @@ hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream) {
                 return e;
             attr = true;
         }
+#if NN_GEMM_VARIANT == 9
+        // persistent: one workgroup per CU (128 KiB of LDS each), each walking its tiles
+        static int nCu = 0;
+        if (nCu == 0) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&nCu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || nCu <= 0)
+                nCu = 256;
+        }
+        const uint32_t grid = std::min<uint32_t>(nwg, static_cast<uint32_t>(nCu));
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(512), kLds, stream, a);
+#else
         hipLaunchKernelGGL(kernel, dim3(nwg), dim3(512), kLds, stream, a);
+#endif
     }
     else {
         hipLaunchKernelGGL(dev::nnGemm, dim3(nwg), dim3(256), 0, stream, a);
