@@ -93,6 +93,8 @@ def parse():
                    help="SURVEY 8(d) ragged variant: K_m ~ U[64, 256] with the same total of densities")
     p.add_argument("--no-best", action="store_true", help="do not write best-density indices")
     p.add_argument("--no-extra-mode", action="store_true", help="do not time the other mode")
+    p.add_argument("--no-density-check", action="store_true",
+                   help="N > 1: skip the density-sharded (config 4, RCCL) check beside the headline")
     p.add_argument("--native-f32", action="store_true",
                    help="fp32 mode on the f32-MFMA kernel instead of the split-f16 kernel")
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -449,6 +451,53 @@ def host_boundary(args, ms, kind, calls=6):
             "d2h_gb_per_s": calls * fpl * ms.n_mixtures * 8 / dt / 1e9}
 
 
+def density_sharded_check(args, ms, ws, rank, local, frames_per_call=4096, calls=8):
+    """Config 4 on the driver's multi-GPU runs (N > 1, default frame-sharded bench): the density-sharded
+    SIMD-diagonal-maximum scorer (rasr_amd.parallel.DensityShardedScorer: 1/N of the densities per rank,
+    RCCL all-reduce(MIN) of the split mixtures' packed keys + all-gather) scores one batch on every rank;
+    rank 0 compares the assembled table with the unsharded scorer bit for bit (scores and best densities),
+    and the path's rate over `calls` calls is reported beside the headline (strong scaling: all ranks score
+    the same frames).  Untimed for `value`; any failure is reported in the record, not raised."""
+    import torch
+    import rasr_amd as ra
+    from rasr_amd import parallel
+    kind = "SIMD-diagonal-maximum"
+    try:
+        dev = torch.device("cuda", local)
+        ds = parallel.DensityShardedScorer(ms, kind, frames_per_call, rank, ws, device=local)
+        frames = torch.from_numpy(ra.synthetic_frames(frames_per_call, args.dim, seed=4242)).to(dev)
+        m_local = ds.scorer.n_mixtures()
+        loc_s = torch.empty((m_local, frames_per_call), dtype=torch.float32, device=dev)
+        loc_b = torch.empty((m_local, frames_per_call), dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        full, fullb = ds.score(frames, loc_s, loc_b, stream)
+        barrier(ws)
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            ds.score(frames, loc_s, loc_b, stream)
+        barrier(ws)
+        dt = max_over_ranks(time.perf_counter() - t0, ws)
+        import torch.distributed as dist
+        coll = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
+        rec = {"scorer": kind, "layout": f"density-sharded x{ws} + {coll} all-reduce(MIN) of split mixtures + "
+                                          f"all-gather", "frames_per_call": frames_per_call,
+               "value": calls * frames_per_call / dt, "unit": "frames/s (all ranks score the same frames)"}
+        if rank == 0:
+            ref = ra.Scorer(ms, kind, max_frames=frames_per_call, device=local)
+            rs = torch.empty((ms.n_mixtures, frames_per_call), dtype=torch.float32, device=dev)
+            rb = torch.empty((ms.n_mixtures, frames_per_call), dtype=torch.int32, device=dev)
+            ref.score_device(frames, rs, rb, stream)
+            torch.cuda.synchronize(dev)
+            same = bool(torch.equal(full.view(torch.int32), rs.view(torch.int32)) and torch.equal(fullb, rb))
+            rec["check"] = "bit-exact vs the unsharded scorer" if same else "MISMATCH vs the unsharded scorer"
+            del ref, rs, rb
+        del ds, frames, loc_s, loc_b, full, fullb
+        torch.cuda.empty_cache()
+        return rec
+    except Exception as e:  # reported, never fatal to the headline line
+        return {"scorer": kind, "error": f"{type(e).__name__}: {e}"[:300]}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -491,6 +540,9 @@ def main():
                         "frames_per_gpu_per_step": r2["frames_per_step"], "frames_per_launch": r2["frames_per_launch"],
                         "timed_region_s": r2["timed_region_s"], "dtype": r2["dtype"],
                         "scorer": MODES[other][0], "roofline": r2["roofline"]}
+    dcheck = None
+    if ws > 1 and args.parallel == "frames" and args.mode in ("fp32", "simd") and not args.no_density_check:
+        dcheck = density_sharded_check(args, ms, ws, rank, local)
     cpu = None
     hb = None
     if rank == 0 and ws == 1 and args.host_boundary == "auto" and not args.mode.startswith("presel"):
@@ -533,6 +585,8 @@ def main():
         }
         if extra:
             line["modes"] = extra
+        if dcheck is not None:
+            line["density_sharded"] = dcheck
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist
