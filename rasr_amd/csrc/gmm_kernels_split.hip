@@ -42,6 +42,13 @@
 #ifndef GMM_SPLIT_MIN_WAVES
 #define GMM_SPLIT_MIN_WAVES 1
 #endif
+#ifndef GMM_SPLIT_PRIO
+#define GMM_SPLIT_PRIO 0  // A/B: 1 = s_setprio(1) over a pipeline step's MFMAs, 0 for the emit
+#endif
+#ifndef GMM_SPLIT_ORDER
+#define GMM_SPLIT_ORDER 0  // A/B: MFMA order of a step; 0 = tile A's chain then tile B's, 1 = the two tiles
+                           // alternate on one frame operand (B fragment shared by consecutive MFMAs)
+#endif
 #ifndef GMM_SPLIT_IL
 #define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
 #endif
@@ -379,8 +386,26 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
                           const f32x4(&prev)[2][NF], uint32_t tPrev, const uint2& C0w, const uint2& C1w,
                           uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) {
-        chain(A0, cur[0]);
-        chain(A1, cur[1]);
+        if (GMM_SPLIT_PRIO)
+            __builtin_amdgcn_s_setprio(1);
+        if constexpr (GMM_SPLIT_ORDER == 1) {
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb) {
+                cur[0][cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                cur[1][cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    cur[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[s], B[cb][s], cur[0][cb], 0, 0, 0);
+                    cur[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[s], B[cb][s], cur[1][cb], 0, 0, 0);
+                }
+        }
+        else {
+            chain(A0, cur[0]);
+            chain(A1, cur[1]);
+        }
         readSel(C0w, TTcur[0]);
         readSel(C1w, TTcur[1]);
         pairEpilogue(prev, tPrev - tBeg, TTprev);
@@ -394,6 +419,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     // the emit of the mixture that ended at tile tNext, if any (a separate block: with the emit inside
     // the interleaved one, the duplicated step needs more than 256 VGPRs)
     const auto finish = [&](uint32_t tNext) {
+        if (GMM_SPLIT_PRIO)
+            __builtin_amdgcn_s_setprio(0);
         if (tNext == tEnd) {
             emit();
             resetBest();
