@@ -46,6 +46,9 @@
 #ifndef GMM_I8_MFMA32
 #define GMM_I8_MFMA32 0  // SIMD / batch-int, one covariance: 32x32x32 MFMA kernel scoreI8Seg32 (else scoreI8Seg)
 #endif
+#ifndef GMM_I8_MFMA32_CB
+#define GMM_I8_MFMA32_CB 4  // scoreI8Seg32: column blocks of 32 frames per wave (4 or 2)
+#endif
 #ifndef GMM_I8_MFMA32_MINS
 #define GMM_I8_MFMA32_MINS 8  // scoreI8Seg32: running minima per column block (8: one per candidate pair of a block)
 #endif
@@ -659,12 +662,14 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 #else
 #define GMM_I8_MFMA32_ATTR
 #endif
-template <int KS, int SEG>
+template <int KS, int SEG, int CB>
 __global__ __launch_bounds__(256) GMM_I8_MFMA32_ATTR void scoreI8Seg32(I8Args a, const uint32_t* __restrict__ mixTileOff,
                                                      float* __restrict__ scores, uint32_t* __restrict__ bestOut) {
-    constexpr int      CB        = 4;                           // column blocks of 32 frames per wave
+    // CB: column blocks of 32 frames per wave (4: 512 frames per workgroup, as scoreI8Seg; 2: 256 frames and
+    // half the registers, for 4 waves per SIMD -- the launcher doubles the frame-tile count)
+    static_assert(CB == 2 || CB == 4, "CB");
     constexpr int      KH        = 2 * KS;                      // 32x32x32 MFMAs per block (K = 32 each)
-    constexpr int      NPL       = 2;                           // results per lane per mixture
+    constexpr int      NPL       = CB / 2;                      // results per lane per mixture
     constexpr int      NB        = GMM_I8_MFMA32_MINS;          // running minima per column block
     constexpr int      kSegTiles = SEG;
     constexpr uint32_t kTileA    = KS * 1024;
@@ -759,13 +764,14 @@ __global__ __launch_bounds__(256) GMM_I8_MFMA32_ATTR void scoreI8Seg32(I8Args a,
             v[cb] = x;
         }
         int res[NPL];
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
 #if GMM_PERMLANE
-        res[0] = swapMin32(v[0], v[1]);
-        res[1] = swapMin32(v[2], v[3]);
+            res[i] = swapMin32(v[2 * i], v[2 * i + 1]);
 #else
-        res[0] = min(hl ? v[1] : v[0], __shfl_xor(hl ? v[0] : v[1], 32));
-        res[1] = min(hl ? v[3] : v[2], __shfl_xor(hl ? v[2] : v[3], 32));
+            res[i] = min(hl ? v[2 * i + 1] : v[2 * i], __shfl_xor(hl ? v[2 * i] : v[2 * i + 1], 32));
 #endif
+        }
         finalizeStoreI8<NPL, kMaybeNone>(a, scores, bestOut, res, mm, frame0, lane, ib, ssOut);
     };
     const std::true_type  kHot{};
@@ -888,8 +894,11 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
         }
 #if GMM_I8_MFMA32
         if constexpr (NF == 8) {
-            hipLaunchKernelGGL((dev::scoreI8Seg32<KS, (KS == 1 ? dev::kSegTiles : 8)>), dim3(grid), dim3(256), 0, s, a,
-                               a.mixTileOff, a.scores, a.best);
+            constexpr int kCb = GMM_I8_MFMA32_CB;
+            I8Args        b   = a;  // frame tiles of 4 x kCb x 32 frames (the host pads to 512)
+            b.nFrameTiles     = a.nFrameTiles * (4 / kCb);
+            hipLaunchKernelGGL((dev::scoreI8Seg32<KS, (KS == 1 ? dev::kSegTiles : 8), kCb>), dim3(grid * (4 / kCb)),
+                               dim3(256), 0, s, b, b.mixTileOff, b.scores, b.best);
             return;
         }
 #endif
