@@ -28,6 +28,7 @@ struct NnGemmArgs {
     int             act;       // nn_activation
     float           gamma;
     int             top;
+    int             swapped;   // top layer computed as C^T (A = activations, B = W^T): set by launchNnGemm
 };
 
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,

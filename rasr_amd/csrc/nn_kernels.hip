@@ -389,6 +389,9 @@ __global__ __launch_bounds__(512) void nnGemm256(NnGemmArgs a) {
 #ifndef NN8_STORE16
 #define NN8_STORE16 1  // hidden-layer epilogue: 16-byte stores (permlane16 exchange) instead of 8-byte (A/B: -3.4 %)
 #endif
+#ifndef NN8_TOP_SWAP
+#define NN8_TOP_SWAP 1  // top layer as C^T (frames x classes): 16-byte stores into the class-major score table
+#endif
 #ifndef NN8_PRIO_MODE
 #define NN8_PRIO_MODE 2  // 0: s_setprio(1) around each MFMA cluster; 1: once for group 1; 2: none (fastest, A/B)
 #endif
@@ -637,6 +640,40 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
                 const uint4 w  = {static_cast<uint32_t>(s0[0]), static_cast<uint32_t>(s1[0]),
                                   static_cast<uint32_t>(s0[1]), static_cast<uint32_t>(s1[1])};
                 *reinterpret_cast<uint4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mst) = w;
+            }
+        }
+        return;
+    }
+#endif
+#if NN8_TOP_SWAP
+    if (a.swapped) {
+        // top layer as C^T: rows are frames, columns classes, so a lane holds 4 consecutive frames of one
+        // class -- one 16-byte store into the class-major score table instead of four 4-byte ones
+        const bool vec = (a.scoreStride & 3u) == 0u && (reinterpret_cast<uintptr_t>(a.scores) & 15u) == 0u;
+        float      bc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t c = n0 + 128u * (j >> 1) + wc * 32u + 16u * (j & 1) + col;
+            bc[j]            = a.bias[c];  // bias has Npad (= padded classes) entries
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t fr = m0 + 128u * (i >> 2) + wr * 64u + 16u * (i & 3) + 4u * g;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t c = n0 + 128u * (j >> 1) + wc * 32u + 16u * (j & 1) + col;
+                if (c >= a.M)
+                    continue;
+                float* const dst = a.scores + static_cast<size_t>(c) * a.scoreStride + fr;
+                const f32x4  v   = {-(acc[i][j][0] + bc[j]), -(acc[i][j][1] + bc[j]), -(acc[i][j][2] + bc[j]),
+                                    -(acc[i][j][3] + bc[j])};
+                if (vec && fr + 3u < a.nFrames)
+                    *reinterpret_cast<f32x4*>(dst) = v;
+                else
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        if (fr + rr < a.nFrames)
+                            dst[rr] = v[rr];
             }
         }
         return;
@@ -910,6 +947,19 @@ hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t 
 hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream) {
     if (a.Mpad % kNnTileM || a.Npad % kNnTileN || a.Kpad % kNnTileK || a.Kpad == 0)
         return hipErrorInvalidValue;  // the kernel reads whole tiles without bounds checks
+#if NN_GEMM_VARIANT == 8 && !NN8_MFMA32 && NN8_TOP_SWAP
+    if (kNnTileM == 256 && a.top && !a.swapped) {
+        // the top layer as C^T = activations . W: the tile rows are frames, so the class-major score table
+        // gets 16-byte stores (nnGemm8p epilogue); bias stays indexed by class (now the column)
+        NnGemmArgs t = a;
+        t.A          = a.B;
+        t.B          = a.A;
+        t.Mpad       = a.Npad;
+        t.Npad       = a.Mpad;
+        t.swapped    = 1;
+        return launchNnGemm(t, stream);
+    }
+#endif
     const uint32_t nwg = (a.Mpad / kNnTileM) * (a.Npad / kNnTileN);
     if (nwg == 0)
         return hipSuccess;
