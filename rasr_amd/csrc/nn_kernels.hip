@@ -26,9 +26,18 @@ typedef float  f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef float  f32x16 __attribute__((ext_vector_type(16)));
 
+#ifndef NN_FAST_SIGMOID
+#define NN_FAST_SIGMOID 1
+#endif
 __device__ __forceinline__ float activate(float x, int act, float gamma) {
     switch (act) {
+#if NN_FAST_SIGMOID
+        // SigmoidLayer; v_rcp_f32 (1 ulp) instead of the IEEE division sequence (~10 VALU per value in an
+        // epilogue the matrix cores wait for): far below the bf16 rounding of the layer output
+        case 1: return __builtin_amdgcn_rcpf(1.0f + __expf(-gamma * x));
+#else
         case 1: return 1.0f / (1.0f + __expf(-gamma * x));  // SigmoidLayer
+#endif
         case 2: return tanhf(x);                           // TanhLayer
         case 3: return x > 0.0f ? x : 0.0f;                // RectifiedLayer
         case 4: return x > 0.0f ? x : __expf(x) - 1.0f;    // ExponentialLinearLayer (alpha 1)
