@@ -26,6 +26,9 @@ typedef float  f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef float  f32x16 __attribute__((ext_vector_type(16)));
 
+#ifndef NN_SIGMOID_FMA
+#define NN_SIGMOID_FMA 1  // hidden-layer sigmoid epilogue: bias and gamma folded into one FMA feeding v_exp_f32
+#endif
 #ifndef NN_FAST_SIGMOID
 #define NN_FAST_SIGMOID 1
 #endif
@@ -633,11 +636,27 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
             const uint32_t mb0 = m0 + 128u * (i >> 2) + wr * 64u + 16u * (i & 3);
             const f32x4    b0  = *reinterpret_cast<const f32x4*>(a.bias + mb0 + 4u * g);
             const f32x4    b1  = *reinterpret_cast<const f32x4*>(a.bias + mb0 + 16u + 4u * g);
+#if NN_SIGMOID_FMA
+            const float sk  = -a.gamma * 1.44269504088896341f;
+            const f32x4 bk0 = b0 * sk, bk1 = b1 * sk;
+#endif
             const uint32_t mst = mb0 + 16u * (g & 1u) + 8u * (g >> 1);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t n = n0 + 128u * (j >> 1) + wc * 32u + 16u * (j & 1) + col;
                 u16x4          v0, v1;
+#if NN_SIGMOID_FMA
+                if (a.act == 1) {
+                    // sigmoid(x + b) = 1 / (1 + 2^((x + b) k)), k = -gamma log2(e): one FMA into the exponent
+                    // (x k + b k) instead of the add, the gamma multiply and __expf's log2(e) multiply
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        v0[rr] = toBf16(__builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][rr], sk, bk0[rr]))));
+                        v1[rr] = toBf16(__builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i + 1][j][rr], sk, bk1[rr]))));
+                    }
+                }
+                else
+#endif
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     v0[rr] = toBf16(activate(acc[i][j][rr] + b0[rr], a.act, a.gamma));

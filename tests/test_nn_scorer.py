@@ -97,6 +97,15 @@ def test_nn_scorer_device_strides_and_errors(gpu):
     sc.score_host(xs, out=table)
     assert _err(table[:, :130], ref) <= 2e-3
     assert (table[:, 130:] == 7.0).all()
+    # the top layer writes 4 frames of a class with one 16-byte store when the table allows it: an odd row
+    # stride (133 floats) and a table starting 4 bytes into its allocation take the 4-byte path
+    big = torch.full((200, 133), 7.0, dtype=torch.float32, device=gpu)
+    view = big[:, 1:]  # row stride 133, first column 4 bytes in
+    sc.score_device(padded, view)
+    torch.cuda.synchronize()
+    b = big.cpu().numpy()
+    assert _err(b[:, 1:131], ref) <= 2e-3
+    assert (b[:, 0] == 7.0).all() and (b[:, 131:] == 7.0).all()
     with pytest.raises(ra.GmmError):
         sc.score_host(ra.synthetic_frames(131, 39, seed=1))  # more than max_frames
     with pytest.raises(ra.GmmError):
