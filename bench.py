@@ -93,6 +93,8 @@ def parse():
                    help="SURVEY 8(d) ragged variant: K_m ~ U[64, 256] with the same total of densities")
     p.add_argument("--no-best", action="store_true", help="do not write best-density indices")
     p.add_argument("--no-extra-mode", action="store_true", help="do not time the other mode")
+    p.add_argument("--nn-activation", default="sigmoid", choices=["sigmoid", "tanh", "relu", "elu", "identity"],
+                   help="--mode nn: hidden-layer activation (config 5 is sigmoid)")
     p.add_argument("--no-density-check", action="store_true",
                    help="N > 1: skip the density-sharded (config 4, RCCL) check beside the headline")
     p.add_argument("--native-f32", action="store_true",
@@ -326,7 +328,7 @@ def run_nn(args, ws, rank, local, launches):
     dev = torch.device("cuda", local)
     fpl = args.frames or FRAMES_PER_LAUNCH
     f_step = fpl * launches
-    layers = nn.synthetic_network(NN_DIMS, "sigmoid", seed=2024)
+    layers = nn.synthetic_network(NN_DIMS, args.nn_activation, seed=2024)
     lp = np.full(NN_DIMS[-1], -np.log(NN_DIMS[-1]), np.float32)
     sc = nn.NnScorer(layers, log_prior=lp, prior_scale=1.0, max_frames=fpl, device=local)
     frames = torch.from_numpy(ra.synthetic_frames(f_step, NN_DIMS[0], seed=1000 + rank)).to(dev)
@@ -519,7 +521,7 @@ def main():
                 "unit": "frames/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": res["dtype"], "data": "synthetic (random-init network, frames N(0,1))",
-                "config": {"workload": "hybrid DNN " + "-".join(map(str, NN_DIMS)) + " sigmoid, 5000 classes",
+                "config": {"workload": "hybrid DNN " + "-".join(map(str, NN_DIMS)) + f" {args.nn_activation}, 5000 classes",
                            "frames_per_gpu_per_step": res["frames_per_step"],
                            "frames_per_launch": res["frames_per_launch"],
                            "parallelism": f"frame-sharded replicas x{ws}"},

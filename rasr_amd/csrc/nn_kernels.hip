@@ -29,6 +29,9 @@ typedef float  f32x16 __attribute__((ext_vector_type(16)));
 #ifndef NN_SIGMOID_FMA
 #define NN_SIGMOID_FMA 1  // hidden-layer sigmoid epilogue: bias and gamma folded into one FMA feeding v_exp_f32
 #endif
+#ifndef NN_FAST_TANH
+#define NN_FAST_TANH 1
+#endif
 #ifndef NN_FAST_SIGMOID
 #define NN_FAST_SIGMOID 1
 #endif
@@ -41,7 +44,13 @@ __device__ __forceinline__ float activate(float x, int act, float gamma) {
 #else
         case 1: return 1.0f / (1.0f + __expf(-gamma * x));  // SigmoidLayer
 #endif
+#if NN_FAST_TANH
+        // TanhLayer as 1 - 2 / (2^(2 log2(e) x) + 1): v_exp_f32 + v_rcp_f32 instead of libm's tanhf (its
+        // absolute error, ~1e-7, is far below the bf16 rounding of the layer output; +-1 and NaN kept)
+        case 2: return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(2.88539008177792681f * x));
+#else
         case 2: return tanhf(x);                           // TanhLayer
+#endif
         case 3: return x > 0.0f ? x : 0.0f;                // RectifiedLayer
         case 4: return x > 0.0f ? x : __expf(x) - 1.0f;    // ExponentialLinearLayer (alpha 1)
         default: return x;                                 // IdentityLayer
