@@ -43,6 +43,9 @@
 #ifndef GMM_I8_EXTRA_LDS
 #define GMM_I8_EXTRA_LDS 0  // A/B only: dynamic LDS bytes added to scoreI8Seg's workgroup (limits workgroups per CU)
 #endif
+#ifndef GMM_I8_SLOTS
+#define GMM_I8_SLOTS 1  // scoreI8Seg: running-minimum registers per column block (1, 2 or 4; 1: -0.7 %)
+#endif
 #ifndef GMM_I8_MFMA32
 #define GMM_I8_MFMA32 0  // SIMD / batch-int, one covariance: 32x32x32 MFMA kernel scoreI8Seg32 (else scoreI8Seg)
 #endif
@@ -172,16 +175,26 @@ __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restri
 // never reaches INT_MAX otherwise (the host bounds every real row's packed value below 2^31 - 2^(ib+1),
 // gmm_prepare.cc), so the scorer's per-mixture emit skips those selects (v_cndmask issues at a
 // quarter of the rate of the other VALU ops).
-template <int NF, bool MAYBE_NONE = true>
+template <int NF, bool MAYBE_NONE = true, int S = 4>
 __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict__ scores, uint32_t* __restrict__ bestOut,
-                                              const int (&best)[NF][4], uint32_t m, uint32_t frame0, int lane, int g,
+                                              const int (&best)[NF][S], uint32_t m, uint32_t frame0, int lane, int g,
                                               int ib, const int (&ssOut)[NF / 4]) {
     constexpr int NPL = NF / 4;
-    // per-mixture reduction: 4 rows in-lane, then a reduce-scatter over the 4 lane groups
+    // per-mixture reduction: the S running minima of a column block in-lane, then a reduce-scatter over
+    // the 4 lane groups
     int v[NF];
 #pragma unroll
-    for (int cb = 0; cb < NF; ++cb)
-        v[cb] = min(min(best[cb][0], best[cb][1]), min(best[cb][2], best[cb][3]));
+    for (int cb = 0; cb < NF; ++cb) {
+        if constexpr (S == 4)
+            v[cb] = min(min(best[cb][0], best[cb][1]), min(best[cb][2], best[cb][3]));
+        else {
+            int x = best[cb][0];
+#pragma unroll
+            for (int r = 1; r < S; ++r)
+                x = min(x, best[cb][r]);
+            v[cb] = x;
+        }
+    }
     int w[NF / 2];  // after the lane^32 step: column blocks cb with bit1 == (g >> 1)
     int res[NPL];   // after the lane^16 step: column block cb = g + 4 i
 #if GMM_PERMLANE
@@ -391,8 +404,11 @@ extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 // (the packed row constant XOR 2^31) and compared unsigned, so OR-ing the sign-extended mask byte of a
 // (frame, density cluster) that the frame did not select makes the all-ones key, which never wins; the
 // segment carries each tile's 16 row offsets into the wave's mask table (gmm_kernels_presel.hip).
+#ifndef GMM_I8_WAVES
+#define GMM_I8_WAVES 4  // scoreI8Seg, one K step: waves per SIMD the register allocation must allow (0 = free)
+#endif
 template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles>
-__global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
+__global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_WAVES : 1) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
                                                    float* __restrict__ scores, uint32_t* __restrict__ bestOut) {
     static_assert(NF == 4 || NF == 8, "NF");
     static_assert(!PRESEL || NF == 4, "preselection masks are 64-frame words");
@@ -521,29 +537,33 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
         else
             return min(x, y);
     };
-    int best[NF][4];
+    // running minima per column block: every key carries its density index, so the 4 row slots of a
+    // lane can share kSlots registers (fewer to reduce and reset at each mixture end)
+    constexpr int kSlots = KS == 1 ? GMM_I8_SLOTS : 4;  // two K steps: 4 (fewer live values to schedule around)
+    static_assert(kSlots == 1 || kSlots == 2 || kSlots == 4, "slots");
+    int best[NF][kSlots];
     const auto resetBest = [&]() {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < kSlots; ++r)
                 best[cb][r] = PRESEL ? -1 : INT_MAX;  // PRESEL: 0xffffffff = biased INT_MAX
     };
     // hot: the end of a mixture with tiles (its minimum is a real row: no INT_MAX case, unless PRESEL)
     const auto emit = [&](uint32_t mm, auto hot) {
         constexpr bool kMaybeNone = PRESEL || !decltype(hot)::value;
         if constexpr (PRESEL) {
-            int unb[NF][4];
+            int unb[NF][kSlots];
 #pragma unroll
             for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
+                for (int r = 0; r < kSlots; ++r)
                     unb[cb][r] = static_cast<int>(static_cast<uint32_t>(best[cb][r]) ^ 0x80000000u);
-            emitMixtureI8<NF, kMaybeNone>(a, scores, bestOut, unb, mm, frame0, lane, g, ib, ssOut);
+            emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, unb, mm, frame0, lane, g, ib, ssOut);
         }
         else {
             if (!(GMM_I8_DIAG & 4) || mm + 1 == m1)
-                emitMixtureI8<NF, kMaybeNone>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
+                emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
         }
     };
     const std::true_type  kHot{};
@@ -606,9 +626,17 @@ __global__ __launch_bounds__(256) void scoreI8Seg(I8Args a, const uint32_t* __re
 #pragma unroll
             for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    best[cb][r] = min2(best[cb][r], min2(cand(accA[cb][r], P0[r], T0w[r], cb),
-                                                         cand(accB[cb][r], P1[r], T1w[r], cb)));
+                for (int r = 0; r < 4; ++r) {
+                    const int ca = cand(accA[cb][r], P0[r], T0w[r], cb), cc = cand(accB[cb][r], P1[r], T1w[r], cb);
+                    if constexpr (kSlots < 4 && !PRESEL) {
+                        // several keys into one register: keep each update one v_min3 (the compiler would
+                        // otherwise reassociate the chain into a tree of two-operand v_min)
+                        int& bs = best[cb][r % kSlots];
+                        asm("v_min3_i32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ca), "v"(cc));
+                    }
+                    else
+                        best[cb][r % kSlots] = min2(best[cb][r % kSlots], min2(ca, cc));
+                }
 #if GMM_I8_INTERLEAVE
 #pragma unroll
             for (int i = 0; i < 2 * NF * KS; ++i) {
