@@ -42,6 +42,9 @@
 #ifndef GMM_SPLIT_MIN_WAVES
 #define GMM_SPLIT_MIN_WAVES 1
 #endif
+#ifndef GMM_SPLIT_SLOTS
+#define GMM_SPLIT_SLOTS 4  // scoreSplit: running-minimum registers per column block (1, 2 or 4)
+#endif
 #ifndef GMM_SPLIT_PRIO
 #define GMM_SPLIT_PRIO 0  // A/B: 1 = s_setprio(1) over a pipeline step's MFMAs, 0 for the emit
 #endif
@@ -166,14 +169,19 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
 // lane l stores frame frame0 + l.  Straight-line code (no branch splits the basic block it is
 // scheduled into): uniform options are arithmetic, the frame bound is the buffer's num_records.
 // ---------------------------------------------------------------------------
-template <bool BEST>
-__device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][4], uint32_t m,
+template <bool BEST, int S>
+__device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][S], uint32_t m,
                                                  uint32_t frame0, int lane, uint32_t g, uint32_t kmask, int eOut,
                                                  float noneScore, float halfScale) {
     uint32_t k[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
-        k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
+        if constexpr (S == 4)
+            k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
+        else if constexpr (S == 2)
+            k[cb] = min(best[cb][0], best[cb][1]);
+        else
+            k[cb] = best[cb][0];
     // groups {g&1, g&1|2} of blocks (0,2) and (1,3): lanes < 32 keep blocks 0, 1, lanes >= 32 blocks 2, 3
     uint32_t w[2], wg[2];
 #pragma unroll
@@ -310,12 +318,14 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     const float noneScore = __fmul_rn(a.outScale, PRESEL ? a.backoff
                                                          : (a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f));
 
-    uint32_t   best[NF][4];
-    const auto resetBest = [&]() {
+    // running minima per column block; the key's tag holds (tile, slot r), so the 4 slots can share registers
+    constexpr int kSlots = PRESEL ? 4 : GMM_SPLIT_SLOTS;
+    uint32_t      best[NF][kSlots];
+    const auto    resetBest = [&]() {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < kSlots; ++r)
                 best[cb][r] = 0xffffffffu;
     };
     const auto chain = [&](const f16x8(&A)[KS], f32x4(&acc)[NF]) {
@@ -356,6 +366,11 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
                     best[cb][r] = umin3(best[cb][r], (__float_as_uint(acc[0][cb][r]) & vmask) | ca,
                                         (__float_as_uint(acc[1][cb][r]) & vmask) | cc);
                 }
+                else if constexpr (kSlots < 4) {
+                    // one v_min3 per update (the compiler would reassociate the chain into two-operand v_min)
+                    uint32_t& bs = best[cb][r % kSlots];
+                    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ka), "v"(kb));
+                }
                 else {
                     best[cb][r] = umin3(best[cb][r], ka, kb);
                 }
@@ -366,7 +381,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     resetBest();
     const auto emit = [&]() {
         if (!(GMM_SPLIT_DIAG & 4) || m + 1 == m1)
-            emitMixtureSplit<BEST>(a, best, m, frame0, lane, g, kmask, eOut, noneScore, 0.5f);
+            emitMixtureSplit<BEST, kSlots>(a, best, m, frame0, lane, g, kmask, eOut, noneScore, 0.5f);
     };
     // after an emit at tile tNext: next mixture, and the empty ones that also end there (rare path)
     const auto advance = [&](uint32_t tNext) {
