@@ -43,6 +43,9 @@
 #ifndef GMM_I8_EXTRA_LDS
 #define GMM_I8_EXTRA_LDS 0  // A/B only: dynamic LDS bytes added to scoreI8Seg's workgroup (limits workgroups per CU)
 #endif
+#ifndef GMM_I8_PRESEL_NIB
+#define GMM_I8_PRESEL_NIB 1  // preselection-batch-int: mask tables as one byte per (cluster, t) + expansion table (-20 %)
+#endif
 #ifndef GMM_I8_SLOTS
 #define GMM_I8_SLOTS 1  // scoreI8Seg: running-minimum registers per column block (1, 2 or 4; 1: -0.7 %)
 #endif
@@ -494,6 +497,33 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
 
     // preselection: this wave's 64-frame mask table [cluster][16] after the segment ring
     uint32_t laneSel = 0;  // byte offset of (wave table, column t = lane & 15)
+#if GMM_I8_PRESEL_NIB
+    // compressed: one byte per (cluster, t) whose bit cb says "frame 16 cb + t did not select the cluster"
+    // (4 KiB per wave instead of 16: 5 workgroups per CU instead of 2), expanded back to the 4-byte mask
+    // word by a 16-entry table after the ring
+    const uint32_t lutOff = 2 * kSegBytes + kDummyBytes;
+    if constexpr (PRESEL) {
+        const uint32_t words = a.nClusters * 16u;
+        if (threadIdx.x < 16u) {
+            const uint32_t n = threadIdx.x;
+            reinterpret_cast<uint32_t*>(lds + lutOff)[n] =
+                    ((n & 1u) ? 0xffu : 0u) | ((n & 2u) ? 0xff00u : 0u) | ((n & 4u) ? 0xff0000u : 0u) | ((n & 8u) ? 0xff000000u : 0u);
+        }
+        const uint32_t tabOff = lutOff + 64u + static_cast<uint32_t>(wave) * words;
+        const i32x4*   src    = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
+        uint32_t*      dst    = reinterpret_cast<uint32_t*>(lds + tabOff);
+        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u) {
+            const i32x4 w = src[i];
+            uint32_t    packed = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)  // bit 0 of each byte (0x00 / 0xff) -> bits 0..3 of the top byte
+                packed |= (((static_cast<uint32_t>(w[j]) & 0x01010101u) * 0x01020408u) >> 24) << (8 * j);
+            dst[i] = packed;
+        }
+        laneSel = tabOff + (static_cast<uint32_t>(lane) & 15u);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the table before the first segment's barrier
+    }
+#else
     if constexpr (PRESEL) {
         const uint32_t words = a.nClusters * 16u;
         const i32x4*   src   = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
@@ -502,6 +532,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             dst[i] = src[i];
         laneSel = 2 * kSegBytes + kDummyBytes + (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
     }
+#endif
     // a tile's row constants (the host biases them by 2^31 for PRESEL) and mask words of this lane's 4 rows,
     // from the tile's 64-byte row-constant block pRow and 32-byte cluster-offset block cRow
     const auto tileRows = [&](const int8_t* pRow, const int8_t* cRow, i32x4& P, uint32_t(&T)[4]) {
@@ -510,10 +541,19 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         if constexpr (PRESEL) {
             const uint2 cw = *reinterpret_cast<const uint2*>(cRow + g * 8);
             const int8_t* tb = lds + laneSel;
+#if GMM_I8_PRESEL_NIB
+            // row offsets are cluster * 64 (the float kernel's word table); the byte table has 16 B per cluster
+            const uint32_t* lut = reinterpret_cast<const uint32_t*>(lds + lutOff);
+            T[0] = lut[*reinterpret_cast<const uint8_t*>(tb + ((cw.x & 0xffffu) >> 2))];
+            T[1] = lut[*reinterpret_cast<const uint8_t*>(tb + (cw.x >> 18))];
+            T[2] = lut[*reinterpret_cast<const uint8_t*>(tb + ((cw.y & 0xffffu) >> 2))];
+            T[3] = lut[*reinterpret_cast<const uint8_t*>(tb + (cw.y >> 18))];
+#else
             T[0] = *reinterpret_cast<const uint32_t*>(tb + (cw.x & 0xffffu));
             T[1] = *reinterpret_cast<const uint32_t*>(tb + (cw.x >> 16));
             T[2] = *reinterpret_cast<const uint32_t*>(tb + (cw.y & 0xffffu));
             T[3] = *reinterpret_cast<const uint32_t*>(tb + (cw.y >> 16));
+#endif
         }
     };
 
@@ -908,7 +948,7 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
         if (a.presel) {  // preselection-batch-int: NF 4, 4-tile segments (ring + 4 mask tables < 80 KiB)
             constexpr int      kSeg  = 4;
             constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 32)) + kI8DummyTileBytes(KS, true);
-            const uint32_t     lds   = kRing + 4u * a.nClusters * 64u;
+            const uint32_t     lds   = GMM_I8_PRESEL_NIB ? kRing + 64u + 4u * a.nClusters * 16u : kRing + 4u * a.nClusters * 64u;
             static bool        attr  = false;
             if (!attr) {
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>),
