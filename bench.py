@@ -464,9 +464,15 @@ def density_sharded_check(args, ms, ws, rank, local, frames_per_call=4096, calls
     import rasr_amd as ra
     from rasr_amd import parallel
     kind = "SIMD-diagonal-maximum"
-    try:
-        dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local)
+    ds, err = None, None
+    try:  # the rank-local part first: a rank that fails here must not leave the others in a collective
         ds = parallel.DensityShardedScorer(ms, kind, frames_per_call, rank, ws, device=local)
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"[:300]
+    if max_over_ranks(0.0 if ds is not None else 1.0, ws) > 0.0:
+        return {"scorer": kind, "error": err or "the density-sharded scorer failed on another rank"}
+    try:
         frames = torch.from_numpy(ra.synthetic_frames(frames_per_call, args.dim, seed=4242)).to(dev)
         m_local = ds.scorer.n_mixtures()
         loc_s = torch.empty((m_local, frames_per_call), dtype=torch.float32, device=dev)
