@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-2 closing GPU session on HEAD: parity tests, smoke, PMC passes (copied into profiles/ on the box so
+# the bench line that follows reports the measured traffic of this kernel build), the default bench line,
+# the rocprofv3 kernel-trace summary of the same command, and the NN bench line.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -3 $OUT/$name.log
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+step pytest 1200 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step pmc_fp32 900 bash scripts/profile_pmc.sh fp32
+step pmc_simd 900 bash scripts/profile_pmc.sh simd
+python scripts/pmc_summary.py $OUT/pmc_fp32 scoreSplit --json $OUT/pmc_fp32.json > /dev/null || exit 1
+python scripts/pmc_summary.py $OUT/pmc_simd scoreI8 --json $OUT/pmc_simd.json > /dev/null || exit 1
+cp $OUT/pmc_fp32.json $OUT/pmc_simd.json profiles/
+step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
+step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off --host-boundary off
+step bench_nn 600 python bench.py --mode nn --steps 20 --warmup 3
+step bench_presel_int 600 python bench.py --mode presel-int --steps 10 --warmup 2 --cpu-baseline off --host-boundary off --no-extra-mode
+step bench_presel_float 600 python bench.py --mode presel-float --steps 10 --warmup 2 --cpu-baseline off --host-boundary off --no-extra-mode
+step bench_d45 600 python bench.py --dim 45 --steps 20 --warmup 3 --cpu-baseline off --host-boundary off
+step bench_ragged 600 python bench.py --ragged --steps 20 --warmup 3 --cpu-baseline off --host-boundary off
+step bench_sum 600 python bench.py --mode sum --steps 20 --warmup 3 --cpu-baseline off --host-boundary off --no-extra-mode
+echo done
