@@ -668,11 +668,15 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int ca = cand(accA[cb][r], P0[r], T0w[r], cb), cc = cand(accB[cb][r], P1[r], T1w[r], cb);
-                    if constexpr (kSlots < 4 && !PRESEL) {
+                    if constexpr (kSlots < 4) {
                         // several keys into one register: keep each update one v_min3 (the compiler would
-                        // otherwise reassociate the chain into a tree of two-operand v_min)
+                        // otherwise reassociate the chain into a tree of two-operand v_min); PRESEL compares
+                        // the biased keys unsigned
                         int& bs = best[cb][r % kSlots];
-                        asm("v_min3_i32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ca), "v"(cc));
+                        if constexpr (PRESEL)
+                            asm("v_min3_u32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ca), "v"(cc));
+                        else
+                            asm("v_min3_i32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ca), "v"(cc));
                     }
                     else
                         best[cb][r % kSlots] = min2(best[cb][r % kSlots], min2(ca, cc));
