@@ -410,6 +410,9 @@ __global__ __launch_bounds__(512) void nnGemm256(NnGemmArgs a) {
 #ifndef NN8_STORE16
 #define NN8_STORE16 1  // hidden-layer epilogue: 16-byte stores (permlane16 exchange) instead of 8-byte (A/B: -3.4 %)
 #endif
+#ifndef NN8_TOP_COLS_FIRST
+#define NN8_TOP_COLS_FIRST 1  // the C^T top layer's tile order: columns (classes) of one frame tile first
+#endif
 #ifndef NN8_TOP_SWAP
 #define NN8_TOP_SWAP 1  // top layer as C^T (frames x classes): 16-byte stores into the class-major score table
 #endif
@@ -428,7 +431,11 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
     const uint32_t     nMT = a.Mpad / T, nNT = a.Npad / T, nwg = nMT * nNT;
     const uint32_t     b = blockIdx.x, xcd = b & 7u, q = nwg / 8u, r = nwg % 8u;
     const uint32_t     id = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (b >> 3);
-    const uint32_t     m0 = (id % nMT) * T, n0 = (id / nMT) * T;
+    // workgroups sharing an XCD take consecutive ids: they sweep the tile rows of one column tile (the
+    // activations of one frame tile stay in that XCD's L2); the top layer run as C^T (frames as rows) sweeps
+    // the columns of one row tile instead, so that its frame tile's activations are the shared operand again
+    const bool         colsFirst = NN8_TOP_COLS_FIRST && a.swapped;
+    const uint32_t     m0 = (colsFirst ? id / nNT : id % nMT) * T, n0 = (colsFirst ? id % nNT : id / nMT) * T;
     const uint32_t     wr = wave >> 2, wc = wave & 3u;
     const uint32_t     nK = a.Kpad / BK;
 
