@@ -61,14 +61,19 @@ __device__ __forceinline__ uint16_t toBf16(float x) {
     return __builtin_bit_cast(uint16_t, static_cast<__bf16>(x));  // v_cvt_pk_bf16_f32, RNE, NaN kept
 }
 
+// one workgroup per frame, two features per thread, one 4-byte store of the bf16 pair (Kpad is a multiple of
+// 64, so the pair never leaves the row; the feature after an odd D is written as 0, the padding's value)
 __global__ __launch_bounds__(256) void nnPrepareInput(const float* __restrict__ frames, uint32_t nFrames,
                                                       uint32_t frameStride, uint32_t D, uint32_t Kpad,
                                                       uint16_t* __restrict__ X) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nFrames * D)
-        return;
-    const uint32_t t = i / D, k = i % D;
-    X[static_cast<size_t>(t) * Kpad + k] = toBf16(frames[static_cast<size_t>(t) * frameStride + k]);
+    const uint32_t t = blockIdx.x;
+    const float*   f = frames + static_cast<size_t>(t) * frameStride;
+    uint32_t*      x = reinterpret_cast<uint32_t*>(X + static_cast<size_t>(t) * Kpad);
+    for (uint32_t k = 2u * threadIdx.x; k < D; k += 512u) {
+        const uint32_t lo = toBf16(f[k]);
+        const uint32_t hi = k + 1u < D ? toBf16(f[k + 1u]) : 0u;
+        x[k / 2u]         = lo | (hi << 16);
+    }
 }
 
 __global__ __launch_bounds__(256) void nnGemm(NnGemmArgs a) {
@@ -983,8 +988,8 @@ hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t 
     const uint32_t n = nFrames * D;
     if (n == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(dev::nnPrepareInput, dim3((n + 255) / 256), dim3(256), 0, stream, frames, nFrames, frameStride,
-                       D, Kpad, X);
+    hipLaunchKernelGGL(dev::nnPrepareInput, dim3(nFrames), dim3(256), 0, stream, frames, nFrames, frameStride, D, Kpad,
+                       X);
     return hipGetLastError();
 }
 
