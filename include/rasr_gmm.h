@@ -87,8 +87,9 @@ typedef struct {
  * class); this flag selects the f32-MFMA kernel instead. */
 #define GMM_FLAG_NATIVE_F32 1u
 /* Tile height of the split-f16 kernel.  By default 32-density tiles (v_mfma_f32_32x32x16_f16, K in
- * steps of 16) are used where they save a K step over 16-density tiles (v_mfma_f32_16x16x32_f16, K in
- * steps of 32) -- e.g. dimension 45 -- and the mixtures have <= 512 densities; these flags force one
+ * steps of 16) are used where they save more than 15 % of K over 16-density tiles (v_mfma_f32_16x16x32_f16,
+ * K in steps of 32; the 32x32 loop holds a lower clock) -- e.g. dimension 9, not 39 or 45 -- and the mixtures
+ * have <= 512 densities, or where a mixture is too large for 16-density tiles; these flags force one
  * height (tests, A/B timing; TILE32 applies only within those limits). */
 #define GMM_FLAG_SPLIT_TILE16 2u
 #define GMM_FLAG_SPLIT_TILE32 4u
