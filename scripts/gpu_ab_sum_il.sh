@@ -1,4 +1,5 @@
 # round 2: diagonal-sum interleave ratios (VALU per MFMA in the two halves of a tile step)
+# (the GMM_SUM_IL1 / GMM_SUM_IL2 switches the variants were built with were removed again after this A/B: no gain)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
