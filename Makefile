@@ -24,7 +24,7 @@ LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
             $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/MixtureSetEstimatorFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
             $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o $(BUILD)/gmm_kernels_shard.o $(BUILD)/gmm_hostio.o \
-            $(BUILD)/gmm_kernels_direct.o
+            $(BUILD)/gmm_kernels_direct.o $(BUILD)/gmm_kernels_layout.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 REFSORT   = $(BUILD)/tests/refsort_test
@@ -56,6 +56,11 @@ $(BUILD)/gmm_kernels_direct.o: $(SRC)/gmm_kernels_direct.hip $(HDRS)
 
 # density-sharded exchange keys (BASELINE config 4)
 $(BUILD)/gmm_kernels_shard.o: $(SRC)/gmm_kernels_shard.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# frame-major host tables (gmm_score_host_ring with GMM_HOST_FRAME_MAJOR)
+$(BUILD)/gmm_kernels_layout.o: $(SRC)/gmm_kernels_layout.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -103,6 +103,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: the CPUs available)")
     p.add_argument("--cpu-frames-per-thread", type=int, default=3000)
     p.add_argument("--host-boundary", choices=["auto", "off"], default="auto")
+    p.add_argument("--extras", choices=["auto", "off"], default="auto",
+                   help="N = 1: device lines at 256/1024/4096 frames per call and the C++ drop-in protocol record")
     return p.parse_args()
 
 
@@ -434,23 +436,150 @@ def cpu_baseline(args, ms):
 
 
 def host_boundary(args, ms, kind, calls=6):
-    """gmm_score_host (host frames in, host score + best tables out, PCIe included) into page-locked tables
-    (rasr_amd.pinned_empty = gmm_host_alloc), the path an RASR caller reading score(e) on the host takes."""
+    """gmm_score_host (host frames in, host tables out, PCIe included) into page-locked tables
+    (rasr_amd.pinned_empty = gmm_host_alloc), the path an RASR caller reading score(e) on the host takes:
+    score + best tables, scores only (best densities kept on the device, GMM_HOST_KEEP_BEST: what the search
+    needs), and scores only frame-major (GMM_HOST_FRAME_MAJOR, the drop-in's own table layout)."""
     import rasr_amd as ra
     fpl = args.frames or FRAMES_PER_LAUNCH
     sc = ra.Scorer(ms, kind, max_frames=fpl)
     frames = ra.synthetic_frames(fpl, args.dim, seed=555)
+    m = sc.n_mixtures()
+    out = ra.pinned_empty((m, fpl), "float32")
+    best = ra.pinned_empty((m, fpl), "uint32")
+    out_fm = ra.pinned_empty((fpl, m), "float32")
+    legs = {
+        "scores_and_best": (lambda: sc.score_host(frames, out=out, best_out=best), 8),
+        "scores_only": (lambda: sc.score_host_ring(frames, 0, fpl, out, keep_best=True), 4),
+        "scores_only_frame_major": (lambda: sc.score_host_ring(frames, 0, fpl, out_fm, keep_best=True,
+                                                                frame_major=True), 4),
+    }
+    rec = {"unit": "frames/s", "scorer": kind, "frames_per_call": fpl,
+           "path": "gmm_score_host / gmm_score_host_ring into page-locked tables (gmm_host_alloc), PCIe-inclusive; "
+                   "not `value`"}
+    for name, (fn, bytes_per) in legs.items():
+        fn()  # warm-up (pipeline streams, transposed tables)
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            fn()
+        dt = time.perf_counter() - t0
+        rec[name] = {"value": calls * fpl / dt, "d2h_gb_per_s": calls * fpl * m * bytes_per / dt / 1e9}
+    rec["value"] = rec["scores_only"]["value"]
+    sc.close()
+    return rec
+
+
+def host_leg_all_ranks(args, ms, kind, ws, rank, local, calls=6):
+    """N > 1: the host-buffer path on every rank at once (one process per GPU reading its scores on the host, the
+    corpus-partition deployment of src/Bliss/CorpusDescription.cc:167-174): concurrent PCIe and host-memory
+    traffic of all ranks.  gmm_score_host_ring, scores only into a page-locked table; barrier-bracketed, the
+    slowest rank's time for the aggregate."""
+    import rasr_amd as ra
+    fpl = args.frames or FRAMES_PER_LAUNCH
+    sc = ra.Scorer(ms, kind, max_frames=fpl, device=local)
+    frames = ra.synthetic_frames(fpl, args.dim, seed=555 + rank)
     out = ra.pinned_empty((sc.n_mixtures(), fpl), "float32")
-    best = ra.pinned_empty((sc.n_mixtures(), fpl), "uint32")
-    sc.score_host(frames, out=out, best_out=best)  # warm-up (pipeline streams, staging)
+    sc.score_host_ring(frames, 0, fpl, out, keep_best=True)  # warm-up
+    barrier(ws)
     t0 = time.perf_counter()
     for _ in range(calls):
-        sc.score_host(frames, out=out, best_out=best)
+        sc.score_host_ring(frames, 0, fpl, out, keep_best=True)
     dt = time.perf_counter() - t0
+    barrier(ws)
     sc.close()
-    return {"value": calls * fpl / dt, "unit": "frames/s", "scorer": kind, "frames_per_call": fpl,
-            "path": "gmm_score_host, pinned score + best tables (gmm_host_alloc), PCIe-inclusive; not `value`",
-            "d2h_gb_per_s": calls * fpl * ms.n_mixtures * 8 / dt / 1e9}
+    return host_leg_record(kind, fpl, calls, dt, ws, rank)
+
+
+def host_leg_record(kind, fpl, calls, dt, ws, rank):
+    """Every rank's rate (all-reduce of a one-hot vector) and the aggregate over the slowest rank's time."""
+    rates = [calls * fpl / dt]
+    dt_max = dt
+    if ws > 1:
+        import torch
+        import torch.distributed as dist
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.zeros(ws + 1, dtype=torch.float64, device=dev)
+        t[rank] = calls * fpl / dt
+        dist.all_reduce(t)
+        m = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        rates, dt_max = [float(x) for x in t[:ws].cpu()], float(m.item())
+        backend = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
+    else:
+        backend = None
+    return {"scorer": kind, "frames_per_call": fpl, "calls_per_rank": calls, "ranks": ws, "backend": backend,
+            "per_rank_frames_per_s": rates, "value": ws * calls * fpl / dt_max, "unit": "frames/s (all ranks)",
+            "path": "gmm_score_host_ring, scores only, page-locked table, every rank at once; not `value`"}
+
+
+def small_batches(args, ms, kind, sizes=(256, 1024, 4096), seconds=0.4):
+    """Device-resident scoring at SURVEY 8(d) config 2's batch sizes: frames/s over back-to-back calls of F frames
+    (wall clock, launch gaps included) and the scorer kernel's average time and roofline fraction."""
+    import torch
+    import rasr_amd as ra
+    dev = torch.device("cuda", 0)
+    out = {}
+    for F in sizes:
+        sc = ra.Scorer(ms, kind, max_frames=F)
+        x = torch.from_numpy(ra.synthetic_frames(F, args.dim, seed=77)).to(dev)
+        sres = torch.empty((sc.n_mixtures(), F), dtype=torch.float32, device=dev)
+        bres = torch.empty((sc.n_mixtures(), F), dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        for _ in range(10):
+            sc.score_device(x, sres, bres, stream)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sc.score_device(x, sres, bres, stream)
+        torch.cuda.synchronize()
+        n = max(20, int(seconds / max(time.perf_counter() - t0, 1e-5)))
+        sc.set_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            sc.score_device(x, sres, bres, stream)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        kms, nl = sc.kernel_time(reset=True)
+        sc.set_timing(False)
+        kms /= max(nl, 1)
+        kernel = sc.main_kernel()
+        peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PRODUCTS if kernel.startswith("scoreSplit") else (
+            PEAK_I8_MFMA_TOPS if kernel.startswith("scoreI8") else PEAK_F32_MFMA_TFLOPS)
+        frac = 2.0 * args.dim * ms.n_entries * F / (kms * 1e-3) / 1e12 / peak
+        out[str(F)] = {"frames_per_s": n * F / dt, "kernel_ms": kms, "kernel": kernel, "roofline_frac": frac,
+                       "calls": n}
+        del sc, x, sres, bres
+        torch.cuda.empty_cache()
+    return out
+
+
+# RASR buffer sizes for the drop-in protocol record and the frames timed at each (about 0.1-0.5 s per size)
+DROP_IN_SIZES = [1, 4, 64, 512, 4096, 32768]
+DROP_IN_FRAMES = [1500, 6000, 65536, 196608, 262144, 327680]
+
+
+def drop_in(args, kind):
+    """The C++ drop-in (Mm::Gpu::GpuBatchFeatureScorer / GpuFeatureScorer) driven through the recognizer protocol at
+    RASR buffer sizes, PCIe and host bookkeeping included: tests/cpp/feature_scorer_driver.cc's bench mode (a child
+    process), consuming every emission's score per frame as FeatureScorerNode does; best densities not read (the
+    search), plus one run reading them (the aligners).  Reported beside the headline, never `value`."""
+    drv = os.path.join(ROOT, "build", "tests", "feature_scorer_driver")
+    if not os.access(drv, os.X_OK):
+        return {"error": f"{drv} not built"}
+    recs = []
+    runs = [(DROP_IN_SIZES, DROP_IN_FRAMES, 0), ([4096], [262144], 1)]
+    for sizes, frames, best in runs:
+        cmd = [drv, "bench", kind, ",".join(map(str, sizes)), ",".join(map(str, frames)), str(args.mixtures),
+               str(args.densities), str(args.dim), str(best)]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        except subprocess.TimeoutExpired:
+            return {"error": "driver timed out", "runs": recs}
+        if r.returncode != 0:
+            return {"error": f"driver exit {r.returncode}: {r.stderr[-300:]}", "runs": recs}
+        recs += [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    return {"scorer": kind, "consumer": "score(e) of every emission per frame (FeatureScorerNode dump)",
+            "runs": [{k: v for k, v in x.items() if k not in ("mixtures", "densities", "dim", "checksum", "type")}
+                     for x in recs]}
 
 
 def density_sharded_check(args, ms, ws, rank, local, frames_per_call=4096, calls=8):
@@ -513,6 +642,13 @@ def main():
     if os.environ.get("RASR_BENCH_LAUNCH_PROBE"):  # tests/test_bench_launcher.py: the ranks, no GPU work
         rec = {"rank": int(os.environ.get("RANK", "0")), "world_size": int(os.environ.get("WORLD_SIZE", "1")),
                "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "gpus": args.gpus}
+        if os.environ.get("RASR_BENCH_PROBE_HOST_LEG") and rec["world_size"] > 1:
+            # the N > 1 host leg's collectives over gloo with a synthetic timing (rank r took (r + 1) / 10 s)
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            rec["host_leg"] = host_leg_record("probe", 1000, 3, (rec["rank"] + 1) / 10.0, rec["world_size"],
+                                              rec["rank"])
+            dist.destroy_process_group()
         with open(os.path.join(os.environ["RASR_BENCH_LAUNCH_PROBE"], f"rank{rec['rank']}.json"), "w") as f:
             json.dump(rec, f)
         return
@@ -553,8 +689,16 @@ def main():
         dcheck = density_sharded_check(args, ms, ws, rank, local)
     cpu = None
     hb = None
+    hb_all = None
+    batches = None
+    dropin = None
     if rank == 0 and ws == 1 and args.host_boundary == "auto" and not args.mode.startswith("presel"):
         hb = host_boundary(args, ms, MODES[args.mode][0])
+    if ws > 1 and args.host_boundary == "auto" and args.mode in ("fp32", "simd") and args.parallel == "frames":
+        hb_all = host_leg_all_ranks(args, ms, MODES[args.mode][0], ws, rank, local)
+    if rank == 0 and ws == 1 and args.extras == "auto" and args.mode in ("fp32", "simd"):
+        batches = {MODES[m][0]: small_batches(args, ms, MODES[m][0]) for m in ("fp32", "simd")}
+        dropin = {MODES[m][0]: drop_in(args, MODES[m][0]) for m in ("fp32", "simd")}
     if rank == 0 and ws == 1 and args.cpu_baseline == "auto":
         cpu = cpu_baseline(args, ms)
     if rank == 0:
@@ -591,6 +735,13 @@ def main():
             "cpu_baseline": cpu,
             "host_boundary": hb,
         }
+        if hb_all is not None:
+            line["host_boundary_all_ranks"] = hb_all
+            line["config"]["process_group"] = {"backend": hb_all["backend"], "ranks": ws}
+        if batches is not None:
+            line["small_batches"] = batches
+        if dropin is not None:
+            line["drop_in_protocol"] = dropin
         if extra:
             line["modes"] = extra
         if dcheck is not None:

@@ -143,6 +143,32 @@ int gmm_score_device(gmm_scorer* scorer, const float* frames, uint32_t n_frames,
 int gmm_score_host(gmm_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
                    float* scores, uint32_t* best_density, uint32_t score_stride);
 
+/* The ring buffer of BatchFeatureScorerBase (features_ / scores_, src/Mm/BatchFeatureScorer.hh:164-198,
+ * fillScoreCache over `length` buffered positions from `featureIndex`, BatchFeatureScorer.cc:98-105) in ONE
+ * call, wrapped or not: the frames are the host rows ring[((first + i) % ring_size) * frame_stride],
+ * i < n_frames (n_frames <= ring_size, first < ring_size), and the results of ring position p go to column p
+ * of the [n_mixtures][score_stride] tables (score_stride >= ring_size).  HOST buffers, synchronous, as
+ * gmm_score_host (which is this call with ring_size = n_frames, first = 0).
+ * flags: GMM_HOST_KEEP_BEST (best_density must be NULL): the best densities are computed but not copied;
+ *   the scorer keeps them on the device until its next host call, and gmm_fetch_best_density copies them
+ *   into the caller's table on demand -- a caller that reads only score(e) (the search) moves 4 instead of
+ *   8 bytes per (frame, mixture) over PCIe, while bestDensity(e) (the aligners) still works.
+ * flags: GMM_HOST_FRAME_MAJOR: the tables are frame-major instead, results of ring position p in ROW p of
+ *   [ring_size][score_stride] (score_stride >= n_mixtures): a caller reading one frame's scores for many
+ *   mixtures (ContextScorer::score(e) of the search, FeatureScorerNode's dump) reads contiguous memory
+ *   instead of one cache line per emission.  The device transposes each chunk before the copy.
+ * *call_id (may be NULL) receives the call's id. */
+#define GMM_HOST_KEEP_BEST 1u
+#define GMM_HOST_FRAME_MAJOR 2u
+int gmm_score_host_ring(gmm_scorer* scorer, const float* ring, uint32_t ring_size, uint32_t first,
+                        uint32_t n_frames, uint32_t frame_stride, float* scores, uint32_t* best_density,
+                        uint32_t score_stride, uint32_t flags, uint64_t* call_id);
+
+/* Best densities of host call `call_id` (made with GMM_HOST_KEEP_BEST) into the same ring positions of
+ * best_density, in the same layout, that its scores went to.  GMM_ERR_INVALID_ARGUMENT once a later
+ * host call of this scorer has replaced them (the caller scores those frames again). */
+int gmm_fetch_best_density(gmm_scorer* scorer, uint64_t call_id, uint32_t* best_density, uint32_t score_stride);
+
 /* Page-locked host memory for gmm_score_host's outputs (the buffer a batched caller keeps, e.g.
  * BatchFeatureScorerBase::scores_, BatchFeatureScorer.hh:177-186), so that callers need no HIP
  * headers.  gmm_host_free(NULL) is a no-op. */

@@ -6,6 +6,7 @@
 #include <Mm/Module.hh>
 
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -40,11 +41,18 @@ void routeCriticalError(const std::string& message) {
     std::abort();
 }
 
+// the library's handler is process-global: installed once (first scorer constructed or registration),
+// never rewritten per call by several recognizer threads
+std::once_flag gHandlerOnce;
+void installCriticalErrorHandler() {
+    std::call_once(gHandlerOnce, [] { Gpu::setCriticalErrorHandler(routeCriticalError); });
+}
+
+// the owner of the calls in this thread (thread_local: no shared state between recognizer threads)
 struct CallScope {
     explicit CallScope(const Core::Component* c)
             : prev_(tOwner) {
         tOwner = c;
-        Gpu::setCriticalErrorHandler(routeCriticalError);
     }
     ~CallScope() {
         tOwner = prev_;
@@ -118,6 +126,7 @@ private:
 GpuFeatureScorer::GpuFeatureScorer(const Core::Configuration& c, Core::Ref<const MixtureSet> mixtureSet,
                                    const char* scorerType)
         : Core::Component(c), Precursor(c) {
+    installCriticalErrorHandler();
     Gpu::Configuration cfg;
     cfg.type               = scorerType;
     cfg.bufferSize         = paramBufferSize(c);
@@ -226,6 +235,7 @@ void registerOne(FeatureScorerFactory* f, u32 firstId) {
 }  // namespace
 
 void Mm::registerGpuFeatureScorers(u32 firstId) {
+    installCriticalErrorHandler();
     FeatureScorerFactory* f = Module::instance().featureScorerFactory();
     registerOne<0>(f, firstId);
     registerOne<1>(f, firstId);

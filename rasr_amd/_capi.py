@@ -88,6 +88,9 @@ class EstimatorConfig(ctypes.Structure):
     ]
 
 
+GMM_HOST_KEEP_BEST = 1
+GMM_HOST_FRAME_MAJOR = 2
+
 # (name, restype, argtypes) for every function declared in include/rasr_gmm.h and rasr_gmm_io.h
 PROTOTYPES = [
     ("gmm_default_config", None, [ctypes.POINTER(ScorerConfig)]),
@@ -105,6 +108,10 @@ PROTOTYPES = [
     ("gmm_score_host", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
       ctypes.c_uint32]),
+    ("gmm_score_host_ring", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
+    ("gmm_fetch_best_density", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]),
     ("gmm_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     ("gmm_host_free", ctypes.c_int, [ctypes.c_void_p]),
     ("gmm_scorer_quantization", ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p]),

@@ -56,6 +56,17 @@ int upload(T** dst, const std::vector<T>& src, size_t padElems = 0) {
     return GMM_OK;
 }
 
+// gmm_score_host_ring: the caller's frames are the rows ring[(first + i) % ringSize], i < nFrames
+struct HostRing {
+    const float* frames;
+    uint32_t     ringSize, first, nFrames, frameStride;
+};
+
+// [t0, t0 + n) of a call, copied to destination columns [col, col + n)
+struct HostSegment {
+    uint32_t chunk, t0, n, col;
+};
+
 struct ChunkTable {
     uint32_t  nChunks = 0;
     uint32_t* dMixOff = nullptr;
@@ -134,6 +145,14 @@ struct gmm_scorer {
     size_t                        hStageBytes  = 0;
     std::unique_ptr<HostCopyPool> copyPool;
     std::map<uint32_t, ChunkTable> chunks;  // keyed by frame tiles per call
+    // host calls (gmm_score_host*): id of the last one; the one whose best densities dHostBest keeps
+    // (GMM_HOST_KEEP_BEST) with its ring mapping and copy segments, for gmm_fetch_best_density
+    uint64_t                 hostCall = 0, keptBestCall = 0;
+    HostRing                 keptRing{};
+    std::vector<HostSegment> keptSegs;
+    bool                     keptFrameMajor = false;
+    float*                   dHostScoresT   = nullptr;  // frame-major copies (GMM_HOST_FRAME_MAJOR)
+    uint32_t*                dHostBestT     = nullptr;
     // kernel timing (gmm_scorer_set_timing)
     bool                                        timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -143,7 +162,7 @@ struct gmm_scorer {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
                         dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
                         dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu, dCentre,
-                        dDirMean, dDirConst, dDirLogNorm, dDirCov};
+                        dDirMean, dDirConst, dDirLogNorm, dDirCov, dHostScoresT, dHostBestT};
         for (void* p : ptrs)
             if (p)
                 (void)hipFree(p);
@@ -479,11 +498,16 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
     return GMM_OK;
 }
 
-// gmm_score_host for large calls (score table >= kHostPipelineBytes).  The batch is scored in frame
-// chunks on hostCompute; the copy-out of chunk k on hostCopy overlaps the scoring of chunk k+1.  A
-// pinned destination is written by the DMA engines directly.  A pageable one goes through a pinned
-// double-buffered staging ring: the D2H of piece j+1 is in flight while the copy threads move piece j
-// into the caller's rows (the runtime's own pageable path is one thread, ~10 GB/s).
+// gmm_score_host / gmm_score_host_ring.  The caller's frames are the rows ring[(first + i) % ringSize],
+// i < nFrames, and the scores of call frame i go to column (first + i) % ringSize of the caller's
+// [nMix][scoreStride] tables (gmm_score_host: ringSize = nFrames, first = 0).  The frames are scored on
+// hostCompute in frame chunks (one chunk for small tables); the copy-out of chunk k on hostCopy overlaps
+// the scoring of chunk k+1.  A chunk that straddles the ring's wrap is copied out as two segments, so every
+// copy has contiguous destination columns.  A pinned destination is written by the DMA engines directly;
+// a pageable one goes through a pinned double-buffered staging ring: the D2H of piece j+1 is in flight
+// while the copy threads move piece j into the caller's rows (the runtime's own pageable path is one
+// thread, ~10 GB/s).  With GMM_HOST_KEEP_BEST the best densities stay in dHostBest (no copy) for
+// gmm_fetch_best_density.
 constexpr size_t   kHostPipelineBytes = size_t(8) << 20;
 constexpr uint32_t kHostChunkFrames   = 8192;
 constexpr uint32_t kHostMaxChunks     = 8;
@@ -520,72 +544,81 @@ int ensureHostStage(gmm_scorer* s, size_t rowBytes) {
     return GMM_OK;
 }
 
-int scoreHostPipelinedImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
-                           uint32_t* best, uint32_t scoreStride) {
-    const uint32_t fpb = framesPerBlock(s);
-    // one chunk for preselection: gmm_scorer_cluster_selection reports the last call's whole batch
-    uint32_t nChunks = s->presel ? 1u : std::clamp<uint32_t>(nFrames / kHostChunkFrames, 1u, kHostMaxChunks);
-    const uint32_t per = ((nFrames + nChunks - 1) / nChunks + fpb - 1) / fpb * fpb;
-    nChunks            = (nFrames + per - 1) / per;
-    int rc             = ensureHostPipeline(s, nChunks);
-    if (rc != GMM_OK)
-        return rc;
-    const size_t D = s->D;
-    // after the legacy stream's earlier work (gmm_score_device callers on stream 0 share the staging)
-    GMM_HIP_CHECK(hipEventRecord(s->hostStart, nullptr));
-    GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCompute, s->hostStart, 0));
-    GMM_HIP_CHECK(hipMemcpy2DAsync(s->dHostFrames, D * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
-                                   D * sizeof(float), nFrames, hipMemcpyHostToDevice, s->hostCompute));
-    for (uint32_t k = 0; k < nChunks; ++k) {
-        const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
-        rc = scoreImpl(s, s->dHostFrames + t0 * D, n, s->D, s->dHostScores + t0, best ? s->dHostBest + t0 : nullptr, nFrames,
-                       s->hostCompute);
-        if (rc != GMM_OK)
-            return rc;
-        GMM_HIP_CHECK(hipEventRecord(s->chunkDone[k], s->hostCompute));
+// the call's frame range [t0, t0 + n) of chunk k, cut at the ring's wrap
+void appendSegments(const HostRing& r, uint32_t k, uint32_t t0, uint32_t n, std::vector<HostSegment>& out) {
+    const uint32_t wrap = r.ringSize - r.first;  // call frame that lands in column 0
+    if (t0 < wrap && t0 + n > wrap) {
+        out.push_back(HostSegment{k, t0, wrap - t0, r.first + t0});
+        out.push_back(HostSegment{k, wrap, t0 + n - wrap, 0});
     }
+    else
+        out.push_back(HostSegment{k, t0, n, t0 < wrap ? r.first + t0 : t0 - wrap});
+}
 
+// device tables -> caller tables at the segments' ring positions, on hostCopy after each segment's chunk;
+// synchronizes hostCopy.  Mixture-major: the device tables [nMix][nFrames] (dHostScores, dHostBest) into
+// columns of [nMix][scoreStride]; frame-major: their transposes [nFrames][nMix] (dHostScoresT, dHostBestT)
+// into rows of [ringSize][scoreStride].
+int copyOutTables(gmm_scorer* s, const std::vector<HostSegment>& segs, uint32_t nFrames, bool frameMajor, float* scores,
+                  uint32_t* best, uint32_t scoreStride) {
     struct Table {
         char*       dst;
         const char* src;
     };
-    std::vector<Table> direct, staged;
-    for (Table t : {Table{reinterpret_cast<char*>(scores), reinterpret_cast<const char*>(s->dHostScores)},
-                    Table{reinterpret_cast<char*>(best), reinterpret_cast<const char*>(s->dHostBest)}})
-        if (t.dst)
-            (isPinnedHost(t.dst) ? direct : staged).push_back(t);
-    const size_t dPitch = static_cast<size_t>(scoreStride) * 4, sPitch = static_cast<size_t>(nFrames) * 4;
-    for (uint32_t k = 0; k < nChunks; ++k) {
-        const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
-        GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCopy, s->chunkDone[k], 0));
-        for (const Table& t : direct)
-            GMM_HIP_CHECK(hipMemcpy2DAsync(t.dst + static_cast<size_t>(t0) * 4, dPitch, t.src + static_cast<size_t>(t0) * 4,
-                                           sPitch, static_cast<size_t>(n) * 4, s->nMix, hipMemcpyDeviceToHost,
-                                           s->hostCopy));
+    struct Copy {  // one 2D copy: `height` rows of `width` bytes
+        uint32_t    chunk;
+        const char* src;
+        size_t      sPitch;
+        char*       dst;
+        size_t      dPitch, width, height;
+    };
+    const char* srcS = reinterpret_cast<const char*>(frameMajor ? s->dHostScoresT : s->dHostScores);
+    const char* srcB = reinterpret_cast<const char*>(frameMajor ? s->dHostBestT : s->dHostBest);
+    std::vector<Copy> direct, staged;
+    const size_t      M = s->nMix, dPitch = static_cast<size_t>(scoreStride) * 4;
+    for (Table t : {Table{reinterpret_cast<char*>(scores), srcS}, Table{reinterpret_cast<char*>(best), srcB}}) {
+        if (!t.dst)
+            continue;
+        const bool pinned = isPinnedHost(t.dst);
+        for (const HostSegment& g : segs) {
+            const Copy c = frameMajor ? Copy{g.chunk, t.src + static_cast<size_t>(g.t0) * M * 4, M * 4,
+                                             t.dst + static_cast<size_t>(g.col) * dPitch, dPitch, M * 4, g.n}
+                                      : Copy{g.chunk, t.src + static_cast<size_t>(g.t0) * 4, static_cast<size_t>(nFrames) * 4,
+                                             t.dst + static_cast<size_t>(g.col) * 4, dPitch, static_cast<size_t>(g.n) * 4, M};
+            if (c.width && c.height)
+                (pinned ? direct : staged).push_back(c);
+        }
+    }
+    for (size_t i = 0; i < direct.size(); ++i) {
+        const Copy& c = direct[i];
+        if (i == 0 || direct[i - 1].chunk != c.chunk)
+            GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCopy, s->chunkDone[c.chunk], 0));
+        GMM_HIP_CHECK(hipMemcpy2DAsync(c.dst, c.dPitch, c.src, c.sPitch, c.width, c.height, hipMemcpyDeviceToHost, s->hostCopy));
     }
     if (!staged.empty()) {
-        if ((rc = ensureHostStage(s, static_cast<size_t>(per) * 4)) != GMM_OK)
+        size_t maxW = 4;
+        for (const Copy& c : staged)
+            maxW = std::max(maxW, c.width);
+        int rc;
+        if ((rc = ensureHostStage(s, maxW)) != GMM_OK)
             return rc;
         struct Piece {
-            uint32_t k, t0, n, r0, r1;
-            Table    t;
+            Copy   c;
+            size_t r0, r1;
         };
         std::vector<Piece> pieces;
-        for (uint32_t k = 0; k < nChunks; ++k) {
-            const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
-            const uint32_t rows = static_cast<uint32_t>(std::max<size_t>(1, s->hStageBytes / (static_cast<size_t>(n) * 4)));
-            for (const Table& t : staged)
-                for (uint32_t r0 = 0; r0 < s->nMix; r0 += rows)
-                    pieces.push_back(Piece{k, t0, n, r0, std::min(s->nMix, r0 + rows), t});
+        for (const Copy& c : staged) {
+            const size_t rows = std::max<size_t>(1, s->hStageBytes / c.width);
+            for (size_t r0 = 0; r0 < c.height; r0 += rows)
+                pieces.push_back(Piece{c, r0, std::min(c.height, r0 + rows)});
         }
         char* stage[2] = {static_cast<char*>(s->hStage), static_cast<char*>(s->hStage) + s->hStageBytes};
         auto  issue    = [&](size_t j) -> int {
             const Piece& p = pieces[j];
-            if (j == 0 || pieces[j - 1].k != p.k)
-                GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCopy, s->chunkDone[p.k], 0));
-            GMM_HIP_CHECK(hipMemcpy2DAsync(stage[j & 1], static_cast<size_t>(p.n) * 4,
-                                           p.t.src + static_cast<size_t>(p.r0) * sPitch + static_cast<size_t>(p.t0) * 4, sPitch,
-                                           static_cast<size_t>(p.n) * 4, p.r1 - p.r0, hipMemcpyDeviceToHost, s->hostCopy));
+            if (j == 0 || pieces[j - 1].c.chunk != p.c.chunk)
+                GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCopy, s->chunkDone[p.c.chunk], 0));
+            GMM_HIP_CHECK(hipMemcpy2DAsync(stage[j & 1], p.c.width, p.c.src + p.r0 * p.c.sPitch, p.c.sPitch, p.c.width,
+                                           p.r1 - p.r0, hipMemcpyDeviceToHost, s->hostCopy));
             GMM_HIP_CHECK(hipEventRecord(s->stageDone[j & 1], s->hostCopy));
             return GMM_OK;
         };
@@ -598,24 +631,119 @@ int scoreHostPipelinedImpl(gmm_scorer* s, const float* frames, uint32_t nFrames,
             GMM_HIP_CHECK(hipEventSynchronize(s->stageDone[j & 1]));
             const Piece& p   = pieces[j];
             const char*  src = stage[j & 1];
-            const size_t w   = static_cast<size_t>(p.n) * 4;
             s->copyPool->parallelFor(p.r1 - p.r0, [&](size_t b, size_t e) {
                 for (size_t r = b; r < e; ++r)
-                    std::memcpy(p.t.dst + (p.r0 + r) * dPitch + static_cast<size_t>(p.t0) * 4, src + r * w, w);
+                    std::memcpy(p.c.dst + (p.r0 + r) * p.c.dPitch, src + r * p.c.width, p.c.width);
             });
         }
     }
     GMM_HIP_CHECK(hipStreamSynchronize(s->hostCopy));
+    return GMM_OK;
+}
+
+// frame-major copies of the device tables' columns [t0, t0 + n) (gmm_kernels_layout.hip)
+int transposeChunk(gmm_scorer* s, bool scores, bool best, uint32_t t0, uint32_t n, uint32_t nFrames) {
+    const uint32_t M = s->nMix;
+    if (scores)
+        GMM_HIP_CHECK(launchTransposeWords(reinterpret_cast<const uint32_t*>(s->dHostScores) + t0, M, n, nFrames,
+                                           reinterpret_cast<uint32_t*>(s->dHostScoresT) + static_cast<size_t>(t0) * M, M,
+                                           s->hostCompute));
+    if (best)
+        GMM_HIP_CHECK(launchTransposeWords(s->dHostBest + t0, M, n, nFrames, s->dHostBestT + static_cast<size_t>(t0) * M, M,
+                                           s->hostCompute));
+    return GMM_OK;
+}
+
+int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, uint32_t scoreStride, bool keepBest,
+                  bool frameMajor) {
+    const uint32_t fpb = framesPerBlock(s), nFrames = r.nFrames;
+    // frame chunks for large tables; one chunk for preselection (gmm_scorer_cluster_selection reports the
+    // last call's whole batch)
+    const bool large   = static_cast<size_t>(nFrames) * std::max<uint32_t>(s->nMix, 1) * sizeof(float) >= kHostPipelineBytes;
+    uint32_t   nChunks = s->presel || !large ? 1u : std::clamp<uint32_t>(nFrames / kHostChunkFrames, 1u, kHostMaxChunks);
+    const uint32_t per = ((nFrames + nChunks - 1) / nChunks + fpb - 1) / fpb * fpb;
+    nChunks            = (nFrames + per - 1) / per;
+    int rc             = ensureHostPipeline(s, nChunks);
+    if (rc != GMM_OK)
+        return rc;
+    std::vector<HostSegment> segs, rows;
+    appendSegments(r, 0, 0, nFrames, rows);  // the frame rows: at most two contiguous runs of the ring
+    for (uint32_t k = 0; k < nChunks; ++k)
+        appendSegments(r, k, k * per, std::min(per, nFrames - k * per), segs);
+    const size_t D = s->D;
+    // after the legacy stream's earlier work (gmm_score_device callers on stream 0 share the staging)
+    GMM_HIP_CHECK(hipEventRecord(s->hostStart, nullptr));
+    GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCompute, s->hostStart, 0));
+    for (const HostSegment& g : rows)
+        GMM_HIP_CHECK(hipMemcpy2DAsync(s->dHostFrames + g.t0 * D, D * sizeof(float),
+                                       r.frames + static_cast<size_t>(g.col) * r.frameStride,
+                                       static_cast<size_t>(r.frameStride) * sizeof(float), D * sizeof(float), g.n,
+                                       hipMemcpyHostToDevice, s->hostCompute));
+    const bool withBest = best || keepBest;
+    for (uint32_t k = 0; k < nChunks; ++k) {
+        const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
+        rc = scoreImpl(s, s->dHostFrames + t0 * D, n, s->D, s->dHostScores + t0, withBest ? s->dHostBest + t0 : nullptr,
+                       nFrames, s->hostCompute);
+        if (rc == GMM_OK && frameMajor)
+            rc = transposeChunk(s, true, best != nullptr, t0, n, nFrames);
+        if (rc != GMM_OK)
+            return rc;
+        GMM_HIP_CHECK(hipEventRecord(s->chunkDone[k], s->hostCompute));
+    }
+    if ((rc = copyOutTables(s, segs, nFrames, frameMajor, scores, best, scoreStride)) != GMM_OK)
+        return rc;
     GMM_HIP_CHECK(hipStreamSynchronize(s->hostCompute));
+    if (keepBest) {
+        s->keptBestCall  = s->hostCall;
+        s->keptRing      = r;
+        s->keptSegs      = segs;
+        s->keptFrameMajor = frameMajor;
+    }
     return GMM_OK;
 }
 
 // On an error after work was queued, wait for both pipeline streams before returning: no DMA into the
 // caller's buffers and no kernel reading dHostFrames may outlive the call (later calls order only against
 // the null stream).
-int scoreHostPipelined(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
-                       uint32_t* best, uint32_t scoreStride) {
-    const int rc = scoreHostPipelinedImpl(s, frames, nFrames, frameStride, scores, best, scoreStride);
+// types with an assignment (AssigningFeatureScorer: SIMD-diagonal-maximum, diagonal-maximum, diagonal-sum)
+bool hasAssignment(const gmm_scorer* s) {
+    return s->flavor == Flavor::Simd || s->flavor == Flavor::DiagonalMaximum || s->flavor == Flavor::DiagonalSum;
+}
+
+int scoreHost(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, uint32_t scoreStride, uint32_t flags,
+              uint64_t* callId) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    if ((flags & ~(GMM_HOST_KEEP_BEST | GMM_HOST_FRAME_MAJOR)) != 0)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "unknown flags");
+    const bool frameMajor = (flags & GMM_HOST_FRAME_MAJOR) != 0;
+    if ((flags & GMM_HOST_KEEP_BEST) && best)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST with a best_density table");
+    const bool keepBest = (flags & GMM_HOST_KEEP_BEST) && hasAssignment(s);  // batch types: nothing to keep
+    // a new host call replaces the best densities a previous one kept
+    s->keptBestCall = 0;
+    const uint64_t id = ++s->hostCall;
+    if (callId)
+        *callId = id;
+    if (r.nFrames == 0)
+        return GMM_OK;
+    if (r.nFrames > s->cfg.max_frames)
+        return fail(GMM_ERR_CAPACITY, "n_frames exceeds config.max_frames");
+    if (!r.frames || !scores || r.frameStride < s->D || r.first >= r.ringSize || r.nFrames > r.ringSize ||
+        scoreStride < (frameMajor ? s->nMix : r.ringSize))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frames/scores/stride/ring");
+    GMM_HIP_CHECK(hipSetDevice(s->device));
+    const size_t maxF = s->cfg.max_frames;
+    if (!s->dHostFrames) {
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostFrames), maxF * s->D * sizeof(float)));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostScores), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(float)));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostBest), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(uint32_t)));
+    }
+    if (frameMajor && !s->dHostScoresT) {
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostScoresT), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(float)));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostBestT), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(uint32_t)));
+    }
+    const int rc = scoreHostImpl(s, r, scores, best, scoreStride, keepBest, frameMajor);
     if (rc != GMM_OK)
         for (hipStream_t st : {s->hostCompute, s->hostCopy})
             if (st)
@@ -847,37 +975,38 @@ int gmm_score_device(gmm_scorer* s, const float* frames, uint32_t nFrames, uint3
 
 int gmm_score_host(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
                    uint32_t* best, uint32_t scoreStride) {
-    if (!s)
-        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
-    if (nFrames == 0)
-        return GMM_OK;
-    if (nFrames > s->cfg.max_frames)
-        return fail(GMM_ERR_CAPACITY, "n_frames exceeds config.max_frames");
-    if (!frames || !scores || frameStride < s->D || scoreStride < nFrames)
-        return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frames/scores/stride");
+    return scoreHost(s, HostRing{frames, std::max<uint32_t>(nFrames, 1), 0, nFrames, frameStride}, scores, best,
+                     scoreStride, 0, nullptr);
+}
+
+int gmm_score_host_ring(gmm_scorer* s, const float* ring, uint32_t ringSize, uint32_t first, uint32_t nFrames,
+                        uint32_t frameStride, float* scores, uint32_t* best, uint32_t scoreStride, uint32_t flags,
+                        uint64_t* callId) {
+    return scoreHost(s, HostRing{ring, ringSize, first, nFrames, frameStride}, scores, best, scoreStride, flags, callId);
+}
+
+int gmm_fetch_best_density(gmm_scorer* s, uint64_t callId, uint32_t* best, uint32_t scoreStride) {
+    if (!s || !best)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    if (!hasAssignment(s))
+        return fail(GMM_ERR_UNSUPPORTED, "scorer type has no best densities (batch types)");
+    if (callId == 0 || callId != s->keptBestCall)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "no best densities kept for this call (a later host call replaced them)");
+    if (scoreStride < (s->keptFrameMajor ? s->nMix : s->keptRing.ringSize))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "score_stride below the call's table layout");
     GMM_HIP_CHECK(hipSetDevice(s->device));
-    const size_t maxF = s->cfg.max_frames;
-    if (!s->dHostFrames) {
-        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostFrames), maxF * s->D * sizeof(float)));
-        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostScores), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(float)));
-        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostBest), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(uint32_t)));
+    int rc = GMM_OK;
+    if (s->keptFrameMajor) {  // transpose the kept best densities now; every chunk's copy waits for it
+        if ((rc = transposeChunk(s, false, true, 0, s->keptRing.nFrames, s->keptRing.nFrames)) != GMM_OK)
+            return rc;
+        for (const HostSegment& g : s->keptSegs)
+            GMM_HIP_CHECK(hipEventRecord(s->chunkDone[g.chunk], s->hostCompute));
     }
-    if (static_cast<size_t>(nFrames) * std::max<uint32_t>(s->nMix, 1) * sizeof(float) >= kHostPipelineBytes)
-        return scoreHostPipelined(s, frames, nFrames, frameStride, scores, best, scoreStride);
-    GMM_HIP_CHECK(hipMemcpy2D(s->dHostFrames, s->D * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
-                              s->D * sizeof(float), nFrames, hipMemcpyHostToDevice));
-    int rc = scoreImpl(s, s->dHostFrames, nFrames, s->D, s->dHostScores, best ? s->dHostBest : nullptr, nFrames, nullptr);
+    // (mixture-major: the call's chunks were complete when it returned, the copies wait on events reached)
+    rc = copyOutTables(s, s->keptSegs, s->keptRing.nFrames, s->keptFrameMajor, nullptr, best, scoreStride);
     if (rc != GMM_OK)
-        return rc;
-    GMM_HIP_CHECK(hipDeviceSynchronize());
-    GMM_HIP_CHECK(hipMemcpy2D(scores, static_cast<size_t>(scoreStride) * sizeof(float), s->dHostScores,
-                              static_cast<size_t>(nFrames) * sizeof(float), static_cast<size_t>(nFrames) * sizeof(float),
-                              s->nMix, hipMemcpyDeviceToHost));
-    if (best)
-        GMM_HIP_CHECK(hipMemcpy2D(best, static_cast<size_t>(scoreStride) * sizeof(uint32_t), s->dHostBest,
-                                  static_cast<size_t>(nFrames) * sizeof(uint32_t),
-                                  static_cast<size_t>(nFrames) * sizeof(uint32_t), s->nMix, hipMemcpyDeviceToHost));
-    return GMM_OK;
+        (void)hipStreamSynchronize(s->hostCopy);
+    return rc;
 }
 
 int gmm_host_alloc(size_t bytes, void** ptr) {

@@ -160,6 +160,10 @@ hipError_t launchPackShardKeys(const float* scores, const uint32_t* best, const 
 hipError_t launchUnpackShardKeys(const int64_t* keys, uint32_t rows, uint32_t nFrames, float* scores, uint32_t* best,
                                  uint32_t stride, hipStream_t stream);
 
+// frame-major host tables (gmm_kernels_layout.hip): dst[c * dstPitch + r] = src[r * srcPitch + c], 32-bit words
+hipError_t launchTransposeWords(const uint32_t* src, uint32_t rows, uint32_t cols, uint32_t srcPitch, uint32_t* dst,
+                                uint32_t dstPitch, hipStream_t stream);
+
 // density preselection (gmm_kernels_presel.hip)
 hipError_t launchAssignDensities(bool quantized, const void* means, uint32_t nDensities, uint32_t Dp,
                                  const void* clusterMeans, uint32_t nClusters, uint8_t* clusterOf, hipStream_t stream);

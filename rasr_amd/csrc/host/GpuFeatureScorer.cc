@@ -185,26 +185,27 @@ std::vector<std::vector<uint8_t>> FeatureScorer::multiplyAndQuantize(const Featu
 // ---------------------------------------------------------------------------
 namespace {
 
-// one frame, all mixtures, owned scores (SimdGaussDiagonalMaximumFeatureScorer::Context)
+// one frame, all mixtures (SimdGaussDiagonalMaximumFeatureScorer::Context): a recycled page-locked slot
 class FrameScorer : public ContextScorer {
 public:
-    FrameScorer(std::vector<float>&& s, std::vector<uint32_t>&& b, bool assigning)
-            : scores_(std::move(s)), best_(std::move(b)), assigning_(assigning) {}
-    EmissionIndex nEmissions() const override { return static_cast<EmissionIndex>(scores_.size()); }
-    Score         score(EmissionIndex e) const override {
-        assert(e < scores_.size());
-        return scores_[e];
-    }
+    FrameScorer(const GpuFeatureScorer* parent, std::unique_ptr<GpuFeatureScorer::Slot> slot,
+                std::shared_ptr<GpuFeatureScorer::SlotPool> pool, EmissionIndex n, bool assigning)
+            : parent_(parent), slot_(std::move(slot)), pool_(std::move(pool)), n_(n), assigning_(assigning) {}
+    ~FrameScorer() override;
+    EmissionIndex nEmissions() const override { return n_; }
+    Score         score(EmissionIndex e) const override;
     bool             hasBestDensity() const override { return assigning_; }
     DensityInMixture bestDensity(EmissionIndex e) const override {
-        assert(e < best_.size());
-        return best_[e];
+        assert(e < n_);
+        return assigning_ ? parent_->slotBestDensity(*slot_, e) : 0xffffffffu;
     }
 
 private:
-    std::vector<float>    scores_;
-    std::vector<uint32_t> best_;
-    bool                  assigning_;
+    const GpuFeatureScorer*                     parent_;
+    std::unique_ptr<GpuFeatureScorer::Slot>     slot_;
+    std::shared_ptr<GpuFeatureScorer::SlotPool> pool_;
+    EmissionIndex                               n_;
+    bool                                        assigning_;
 };
 
 // BatchFeatureScorerBase::ContextScorer (BatchFeatureScorer.hh:42-60)
@@ -230,21 +231,74 @@ private:
 // ---------------------------------------------------------------------------
 // GpuFeatureScorer
 // ---------------------------------------------------------------------------
+struct GpuFeatureScorer::Slot {
+    HostTable<float>    scores;  // [nMixtures]
+    HostTable<uint32_t> best;    // [nMixtures]
+    std::vector<float>  frame;   // the frame, for scoring it again
+    uint64_t            call = 0;
+    bool                bestValid = false;
+};
+
+struct GpuFeatureScorer::SlotPool {
+    std::vector<std::unique_ptr<Slot>> free;
+};
+
+FrameScorer::~FrameScorer() {
+    pool_->free.push_back(std::move(slot_));
+}
+
+Score FrameScorer::score(EmissionIndex e) const {
+    assert(e < n_);
+    return slot_->scores[e];
+}
+
 std::unique_ptr<GpuFeatureScorer> GpuFeatureScorer::create(const MixtureSet& ms, const Configuration& c,
                                                            std::string* error) {
     std::unique_ptr<GpuFeatureScorer> s(new GpuFeatureScorer());
     if (!s->init(ms, c, 1, error))
         return nullptr;
+    s->pool_ = std::make_shared<SlotPool>();
     return s;
 }
 
+GpuFeatureScorer::~GpuFeatureScorer() {}
+
 Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
     assert(f.size() == dimension_);  // require(featureVector.size() == dimension()), SimdFeatureScorer.cc:26
-    std::vector<float>    s(nMixtures_);
-    std::vector<uint32_t> b(nMixtures_);
-    if (gmm_score_host(handle_, f.data(), 1, dimension_, s.data(), assigning_ ? b.data() : nullptr, 1) != GMM_OK)
-        criticalError("gmm_score_host");
-    return std::make_shared<FrameScorer>(std::move(s), std::move(b), assigning_);
+    std::unique_ptr<Slot> slot;
+    if (!pool_->free.empty()) {
+        slot = std::move(pool_->free.back());
+        pool_->free.pop_back();
+    }
+    else {
+        slot.reset(new Slot());
+        const size_t n = std::max<uint32_t>(nMixtures_, 1);
+        if (!slot->scores.allocate(n, 0.0f) || (assigning_ && !slot->best.allocate(n, 0xffffffffu)))
+            criticalError("gmm_host_alloc");
+    }
+    slot->frame.assign(f.begin(), f.end());
+    ++launches_;
+    if (gmm_score_host_ring(handle_, slot->frame.data(), 1, 0, 1, dimension_, slot->scores.data(), nullptr, 1,
+                            assigning_ ? GMM_HOST_KEEP_BEST : 0u, &slot->call) != GMM_OK)
+        criticalError("gmm_score_host_ring");
+    slot->bestValid = false;
+    return std::make_shared<FrameScorer>(this, std::move(slot), pool_, nMixtures_, assigning_);
+}
+
+DensityInMixture GpuFeatureScorer::slotBestDensity(Slot& slot, EmissionIndex e) const {
+    if (!slot.bestValid) {
+        // the device still holds them if no later frame was scored; otherwise score this frame again
+        // (bit-identical scores, its best densities copied directly)
+        if (gmm_fetch_best_density(handle_, slot.call, slot.best.data(), 1) == GMM_OK)
+            ++bestFetches_;
+        else {
+            ++launches_;
+            if (gmm_score_host(handle_, slot.frame.data(), 1, dimension_, slot.scores.data(), slot.best.data(), 1) != GMM_OK)
+                criticalError("gmm_score_host");
+        }
+        slot.bestValid = true;
+    }
+    return slot.best[e];
 }
 
 // ---------------------------------------------------------------------------
@@ -257,14 +311,16 @@ std::unique_ptr<GpuBatchFeatureScorer> GpuBatchFeatureScorer::create(const Mixtu
     if (!s->init(ms, c, b, error))
         return nullptr;
     s->bufferSize_ = b;
-    s->features_.assign(static_cast<size_t>(b) * s->dimension_, 0.0f);
     const size_t n = std::max<size_t>(1, static_cast<size_t>(s->nMixtures_) * b);
-    if (!s->scores_.allocate(n, 0.0f) || (s->assigning_ && !s->best_.allocate(n, 0xffffffffu))) {
+    if (!s->features_.allocate(static_cast<size_t>(b) * std::max<uint32_t>(s->dimension_, 1), 0.0f) ||
+        !s->scores_.allocate(n, 0.0f) || (s->assigning_ && !s->best_.allocate(n, 0xffffffffu))) {
         if (error)
             *error = gmm_last_error();
         return nullptr;
     }
     s->cached_.assign(b, 0);
+    s->bestCached_.assign(b, 0);
+    s->bestCall_.assign(b, 0);
     return s;
 }
 
@@ -277,7 +333,7 @@ void GpuBatchFeatureScorer::reset() const {
 
 void GpuBatchFeatureScorer::setFeature(size_t pos, const FeatureVector& f) const {
     assert(pos < bufferSize_ && f.size() == dimension_);
-    std::copy(f.begin(), f.end(), features_.begin() + pos * dimension_);
+    std::copy(f.begin(), f.end(), features_.data() + pos * dimension_);
 }
 
 // BatchFeatureScorerBase::addFeature, BatchFeatureScorer.cc:46-50
@@ -312,23 +368,23 @@ Scorer GpuBatchFeatureScorer::flush() const {
 }
 
 // Score all mixtures of the buffered positions featureIndex .. featureIndex+length-1 (mod buffer)
-// and cache them (the reference's fillScoreCache does one mixture at a time).  The positions form at
-// most two contiguous runs of the ring; each run is one gmm_score_host call that reads its rows of
-// features_ and writes its columns of the page-locked [nMixtures][bufferSize] tables in place.
+// and cache them (the reference's fillScoreCache does one mixture at a time): one gmm_score_host_ring call
+// reads those rows of features_ and writes their rows of the page-locked frame-major tables in place,
+// wrapped or not.
 void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
     const uint32_t b = bufferSize_;
     length           = std::min(length, b);
-    uint32_t p = featureIndex % b, left = length;
-    while (left > 0) {
-        const uint32_t n = std::min(left, b - p);
-        ++launches_;
-        if (gmm_score_host(handle_, features_.data() + static_cast<size_t>(p) * dimension_, n, dimension_,
-                           scores_.data() + p, assigning_ ? best_.data() + p : nullptr, b) != GMM_OK)
-            criticalError("gmm_score_host");
-        for (uint32_t i = 0; i < n; ++i)
-            cached_[p + i] = 1;
-        left -= n;
-        p = (p + n) % b;
+    const uint32_t p = featureIndex % b;
+    uint64_t       call = 0;
+    ++launches_;
+    if (gmm_score_host_ring(handle_, features_.data(), b, p, length, dimension_, scores_.data(), nullptr, rowStride(),
+                            GMM_HOST_FRAME_MAJOR | (assigning_ ? GMM_HOST_KEEP_BEST : 0u), &call) != GMM_OK)
+        criticalError("gmm_score_host_ring");
+    for (uint32_t i = 0; i < length; ++i) {
+        const uint32_t q = (p + i) % b;
+        cached_[q]       = 1;
+        bestCached_[q]   = 0;
+        bestCall_[q]     = call;
     }
 }
 
@@ -338,15 +394,37 @@ Score GpuBatchFeatureScorer::getScore(EmissionIndex e, uint32_t featureIndex, ui
     const uint32_t p = featureIndex % bufferSize_;
     if (!cached_[p])
         fill(featureIndex, length);
-    return scores_[static_cast<size_t>(e) * bufferSize_ + p];
+    return scores_[static_cast<size_t>(p) * rowStride() + e];
 }
 
 DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {
     assert(e < nMixtures_);
+    if (!assigning_)
+        return 0xffffffffu;
     const uint32_t p = featureIndex % bufferSize_;
     if (!cached_[p])
         fill(featureIndex, length);
-    return best_[static_cast<size_t>(e) * bufferSize_ + p];
+    if (!bestCached_[p]) {
+        const uint64_t call = bestCall_[p];
+        if (gmm_fetch_best_density(handle_, call, best_.data(), rowStride()) == GMM_OK) {
+            ++bestFetches_;  // every position of that call
+            for (uint32_t q = 0; q < bufferSize_; ++q)
+                if (cached_[q] && bestCall_[q] == call)
+                    bestCached_[q] = 1;
+        }
+        else {
+            // a later fill replaced them on the device: score this position again (its row of features_ is
+            // unchanged while cached_[p] holds), best densities copied directly
+            uint64_t again = 0;
+            ++launches_;
+            if (gmm_score_host_ring(handle_, features_.data(), bufferSize_, p, 1, dimension_, scores_.data(), best_.data(),
+                                    rowStride(), GMM_HOST_FRAME_MAJOR, &again) != GMM_OK)
+                criticalError("gmm_score_host_ring");
+            bestCall_[p] = again;
+        }
+        bestCached_[p] = 1;
+    }
+    return best_[static_cast<size_t>(p) * rowStride() + e];
 }
 
 // ---------------------------------------------------------------------------

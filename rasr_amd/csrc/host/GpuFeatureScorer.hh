@@ -164,15 +164,31 @@ protected:
 };
 
 // Unbuffered scorer: every getScorer() scores one frame against all mixtures on the GPU
-// (the SIMD / diagonal-maximum scorers' Context, SimdFeatureScorer.cc:22-35).
+// (the SIMD / diagonal-maximum scorers' Context, SimdFeatureScorer.cc:22-35).  The contexts' tables are
+// page-locked slots recycled when the caller drops a context (no allocation per frame); best densities
+// stay on the device until bestDensity() asks for them (gmm_fetch_best_density), or -- after a later
+// frame replaced them there -- that frame is scored again.  Contexts refer to their scorer, which must
+// outlive them (as the reference's Context refers to its featureScorer_, SimdFeatureScorer.hh:51-68).
 class GpuFeatureScorer : public FeatureScorer {
 public:
     static std::unique_ptr<GpuFeatureScorer> create(const MixtureSet& ms, const Configuration& c,
                                                      std::string* error = nullptr);
+    ~GpuFeatureScorer() override;
     Scorer getScorer(const FeatureVector& f) const override;
+
+    struct Slot;     // a context's page-locked tables and frame
+    struct SlotPool; // the free slots (shared with the contexts that return them)
+
+    // host calls so far (tests: bestDensity() of the newest context copies, an older one re-scores)
+    uint32_t nLaunches() const { return launches_; }
+    uint32_t nBestFetches() const { return bestFetches_; }
+    // bestDensity of a context whose slot is `slot` (ContextScorer side)
+    DensityInMixture slotBestDensity(Slot& slot, EmissionIndex e) const;
 
 private:
     GpuFeatureScorer() {}
+    std::shared_ptr<SlotPool> pool_;
+    mutable uint32_t          launches_ = 0, bestFetches_ = 0;
 };
 
 // Buffered scorer: the BatchFeatureScorerBase ring-buffer protocol (BatchFeatureScorer.cc:40-116).
@@ -192,26 +208,36 @@ public:
     uint32_t bufferSize() const override { return bufferSize_; }
 
     Score            getScore(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
+    // 0xffffffff for the batch types, which have no assignment (as ContextScorer::bestDensity)
     DensityInMixture getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
 
-    // number of GPU launches so far (tests check that one launch serves a whole buffer)
+    // number of GPU launches so far (tests check that one launch serves a whole buffer, wrapped or not)
     uint32_t nLaunches() const { return launches_; }
+    uint32_t nBestFetches() const { return bestFetches_; }
 
 private:
     GpuBatchFeatureScorer() {}
-    void setFeature(size_t pos, const FeatureVector& f) const;
-    void fill(uint32_t featureIndex, uint32_t length) const;
+    void     setFeature(size_t pos, const FeatureVector& f) const;
+    void     fill(uint32_t featureIndex, uint32_t length) const;
+    uint32_t rowStride() const { return nMixtures_ ? nMixtures_ : 1; }
 
-    uint32_t                      bufferSize_ = 4;
-    mutable std::vector<float>    features_;   // [bufferSize][dimension] ring, row = buffer position
-    // [nMixtures][bufferSize] (BatchFeatureScorer.hh:177-186), page-locked: a fill writes the columns of
-    // its buffer positions straight from the device (score stride = bufferSize), no staging copy
-    HostTable<float>              scores_;
-    HostTable<uint32_t>           best_;
-    mutable std::vector<char>     cached_;     // [bufferSize] (all mixtures of a position at once)
-    mutable int32_t               currentFeature_ = 0;
-    mutable int32_t               buffered_       = 0;
-    mutable uint32_t              launches_       = 0;
+    uint32_t bufferSize_ = 4;
+    // [bufferSize][dimension] ring, row = buffer position (BatchFeatureScorerBase::features_), and the
+    // score / best tables, all page-locked: a fill is ONE gmm_score_host_ring call over the buffered
+    // positions, wrapped or not, whose frames and score rows move by DMA directly.  The tables are
+    // frame-major, [bufferSize][nMixtures] (the reference's scores_ is [nMixtures][bufferSize],
+    // BatchFeatureScorer.hh:177-186, filled one mixture at a time): a context's score(e) calls walk one
+    // contiguous row instead of one cache line per emission.  Best densities (assigning types) stay on
+    // the device until bestDensity() asks for them: a score-only caller moves 4 B per (frame, mixture), not 8.
+    HostTable<float>          features_;
+    HostTable<float>          scores_;
+    HostTable<uint32_t>       best_;
+    mutable std::vector<char> cached_;       // [bufferSize] scores of the position are in scores_
+    mutable std::vector<char> bestCached_;   // [bufferSize] best densities of the position are in best_
+    mutable std::vector<uint64_t> bestCall_; // [bufferSize] host call that scored the position
+    mutable int32_t           currentFeature_ = 0;
+    mutable int32_t           buffered_       = 0;
+    mutable uint32_t          launches_       = 0, bestFetches_ = 0;
 };
 
 // Factory by reference type name ("SIMD-diagonal-maximum", "diagonal-maximum",

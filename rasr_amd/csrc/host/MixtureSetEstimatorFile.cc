@@ -309,6 +309,10 @@ int gmm_mixture_set_estimate(const void* data, uint64_t size, const gmm_estimato
         const Accumulator& a = covs[c];
         if (a.weight == 0)  // new DiagonalCovariance(size): variances 1
             continue;
+        // GaussDensityEstimator / CovarianceEstimator: verify(accumulator_.weight() > 0) (GaussDensityEstimator.cc:216)
+        if (!(a.weight > 0) || !std::isfinite(a.weight))
+            return fail(GMM_ERR_INVALID_ARGUMENT, "covariance " + std::to_string(c) + " has weight " +
+                                                          std::to_string(a.weight) + " (verify(weight > 0) failed)");
         std::vector<double> wmss(D, 0.0);  // WeighedMeanSquareSum: x + y * y / meanWeight
         double              wmssWeight = 0;
         for (uint32_t mi : meanSet[c]) {

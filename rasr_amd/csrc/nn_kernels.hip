@@ -45,14 +45,22 @@ __device__ __forceinline__ float activate(float x, int act, float gamma) {
         case 1: return 1.0f / (1.0f + __expf(-gamma * x));  // SigmoidLayer
 #endif
 #if NN_FAST_TANH
-        // TanhLayer as 1 - 2 / (2^(2 log2(e) x) + 1): v_exp_f32 + v_rcp_f32 instead of libm's tanhf (its
-        // absolute error, ~1e-7, is far below the bf16 rounding of the layer output; +-1 and NaN kept)
-        case 2: return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(2.88539008177792681f * x));
+        // TanhLayer as 1 - 2 / (2^(2 log2(e) x) + 1): v_exp_f32 + v_rcp_f32 instead of libm's tanhf.  That form
+        // has an absolute error of ~1e-7, which near 0 is a large RELATIVE error (bf16 keeps small outputs to
+        // 2^-9 relative), so |x| < 2^-4 takes x (1 - x^2 / 3) (the next term, 2 x^5 / 15, is < 2.1e-6 relative);
+        // +-1 and NaN kept
+        case 2: {
+            const float x2 = x * x;
+            return fabsf(x) < 0.0625f ? x * fmaf(x2, -0.333333343f, 1.0f)
+                                      : 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(2.88539008177792681f * x));
+        }
 #else
         case 2: return tanhf(x);                           // TanhLayer
 #endif
         case 3: return x > 0.0f ? x : 0.0f;                // RectifiedLayer
-        case 4: return x > 0.0f ? x : __expf(x) - 1.0f;    // ExponentialLinearLayer (alpha 1)
+        // ExponentialLinearLayer (alpha 1): the reference's own form, alpha (exp(x) - 1) in T
+        // (Math::FastMatrix::elu, src/Math/FastMatrix.hh:1656-1665), cancellation near 0- included
+        case 4: return x > 0.0f ? x : __expf(x) - 1.0f;
         default: return x;                                 // IdentityLayer
     }
 }

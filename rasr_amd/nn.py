@@ -147,10 +147,15 @@ class NnScorer:
         """nn_score_host.  frames: [F][>= input_dim] f32 rows (row stride = frames.shape[1]); out: optional
         caller-kept [n_classes][>= F] table (row stride = out.shape[1]), only its first F columns are written."""
         frames = np.ascontiguousarray(frames, dtype=np.float32)
+        if frames.ndim != 2 or frames.shape[1] < self.input_dim():
+            raise ValueError("frames must be a 2-d f32 [n_frames][>= input_dim] array")
         f = frames.shape[0] if n_frames is None else int(n_frames)
+        if not 0 <= f <= frames.shape[0]:
+            raise ValueError(f"n_frames {f} outside [0, {frames.shape[0]}] (the rows of frames)")
         scores = np.empty((self.n_classes(), f), dtype=np.float32) if out is None else out
-        if scores.dtype != np.float32 or not scores.flags.c_contiguous or scores.ndim != 2 or scores.shape[1] < f:
-            raise ValueError("out must be a C-contiguous f32 [n_classes][>= n_frames] array")
+        if (scores.dtype != np.float32 or not scores.flags.c_contiguous or scores.ndim != 2
+                or scores.shape[0] < self.n_classes() or scores.shape[1] < f):
+            raise ValueError("out must be a C-contiguous f32 [>= n_classes][>= n_frames] array")
         _check(self._l.nn_score_host(self._h, frames.ctypes.data_as(ctypes.c_void_p), f, frames.shape[1],
                                      scores.ctypes.data_as(ctypes.c_void_p), scores.shape[1]), "nn_score_host")
         return scores

@@ -152,6 +152,39 @@ class Scorer:
         _capi.check(rc, "gmm_score_host")
         return scores, best
 
+    def score_host_ring(self, ring: np.ndarray, first: int, n_frames: int, out: np.ndarray,
+                        best_out: np.ndarray | None = None, keep_best: bool = False, frame_major: bool = False) -> int:
+        """gmm_score_host_ring: frames ring[(first + i) % R], i < n_frames (R = ring.shape[0]) into the ring
+        positions of out / best_out: columns of [n_mixtures][>= R] tables, or with frame_major rows of
+        [>= R][>= n_mixtures] tables.  keep_best: best densities stay on the device for fetch_best().
+        Returns the call id."""
+        ring = np.ascontiguousarray(ring, dtype=np.float32)
+        m, R = self.n_mixtures(), ring.shape[0]
+        for name, a, dt in (("out", out, np.float32), ("best_out", best_out, np.uint32)):
+            if a is None:
+                continue
+            ok = a.dtype == dt and a.ndim == 2 and a.flags.c_contiguous and (
+                (a.shape[0] >= R and a.shape[1] >= m) if frame_major else (a.shape[0] == m and a.shape[1] >= R))
+            if not ok:
+                raise ValueError(f"{name} must be a C-contiguous {np.dtype(dt).name} table of the ring's layout")
+        if best_out is not None and best_out.shape[1] != out.shape[1]:
+            raise ValueError("out and best_out must have the same row stride")
+        cid = ctypes.c_uint64()
+        flags = (_capi.GMM_HOST_KEEP_BEST if keep_best else 0) | (_capi.GMM_HOST_FRAME_MAJOR if frame_major else 0)
+        rc = self._lib.gmm_score_host_ring(
+            self._h, ring.ctypes.data_as(ctypes.c_void_p), R, int(first), int(n_frames), ring.shape[1],
+            out.ctypes.data_as(ctypes.c_void_p), best_out.ctypes.data_as(ctypes.c_void_p) if best_out is not None else None,
+            out.shape[1], flags, ctypes.byref(cid))
+        _capi.check(rc, "gmm_score_host_ring")
+        return cid.value
+
+    def fetch_best(self, call_id: int, best_out: np.ndarray) -> None:
+        """gmm_fetch_best_density into the same ring columns the call's scores went to."""
+        if best_out.dtype != np.uint32 or best_out.ndim != 2 or not best_out.flags.c_contiguous:
+            raise ValueError("best_out must be a C-contiguous uint32 table of the call's layout")
+        _capi.check(self._lib.gmm_fetch_best_density(self._h, int(call_id), best_out.ctypes.data_as(ctypes.c_void_p),
+                                                     best_out.shape[1]), "gmm_fetch_best_density")
+
     def set_timing(self, enable: bool) -> None:
         _capi.check(self._lib.gmm_scorer_set_timing(self._h, int(bool(enable))), "gmm_scorer_set_timing")
 

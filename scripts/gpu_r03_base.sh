@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-3 opening GPU session: parity tests, smoke and the default bench line on this round's first box.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r03_base
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -3 $OUT/$name.log
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+step pytest 1100 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
+echo done

@@ -5,6 +5,10 @@
 // usage: feature_scorer_driver <model> <frames.bin> <out.bin> <type> <bufferSize> <segments> [protocol]
 //   protocol  : "recognizer" (default): Speech::OfflineRecognizer, reset() before every segment,
 //               scores as the search reads them;
+//               "delayed": as "recognizer", but every context is consumed only after the next `kDelay`
+//               frames were scored (a RecognizerDelayHandler-like consumer, src/Speech/DelayedRecognizer.cc:65-135;
+//               unbuffered types: bestDensity() of such a context finds its best densities replaced on
+//               the device and scores its frame again);
 //               "node": Speech::FeatureScorerNode::work (src/Speech/FeatureScorerNode.cc:113-162), the
 //               reference's score dump: every frame's -score(e) for ALL emissions (putData, :95-111),
 //               finalize() and reset() after every segment
@@ -16,8 +20,11 @@
 //   frames.bin: u32 F, D; f32 frames[F*D]
 //   out.bin   : u32 F, M, launches; f32 scores[F*M] (frame-major, as consumed); u32 best[F*M]
 // The frames are split into `segments` equal speech segments with reset() between them.
+#include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -58,15 +65,150 @@ static std::unique_ptr<Mm::Gpu::MixtureSet> readBinaryModel(const std::string& p
     return ms;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// bench mode: the drop-in's throughput through the recognizer protocol, PCIe included
+//   feature_scorer_driver bench <type> <bufferSizes> <frames> <mixtures> <densitiesPerMixture> <dim> <best 0|1>
+// bufferSizes / frames: comma-separated lists of equal length (one scorer per buffer size, timed on that many
+// frames).  Synthetic model of SURVEY 8(d) (means N(0,1), pooled variance 0.5 + |N(0,1)|, uniform weights;
+// splitmix64 + Box-Muller) and N(0,1) frames.  Every frame's context is consumed as FeatureScorerNode dumps
+// it: score(e) for every emission (and bestDensity(e) for every emission with best = 1, the aligners' read).
+// One warm-up segment, then one timed segment per size; prints one JSON line per size.
+// ---------------------------------------------------------------------------------------------------------
+namespace {
+struct Rng {
+    uint64_t x;
+    uint64_t next() {
+        uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+        z          = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z          = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        return z ^ (z >> 31);
+    }
+    double uniform() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+    float  normal() {
+        const double u = uniform() + 1e-300, v = uniform();
+        return static_cast<float>(std::sqrt(-2.0 * std::log(u)) * std::cos(6.283185307179586 * v));
+    }
+};
+
+std::vector<uint32_t> parseList(const char* s) {
+    std::vector<uint32_t> out;
+    for (const char* p = s; *p;) {
+        char* end = nullptr;
+        out.push_back(static_cast<uint32_t>(strtoul(p, &end, 10)));
+        p = *end == ',' ? end + 1 : end;
+        if (end == p && *p)
+            break;
+    }
+    return out;
+}
+}  // namespace
+
+static int benchMain(int argc, char** argv) {
+    if (argc != 9) {
+        fprintf(stderr, "usage: %s bench type bufferSizes frames mixtures densitiesPerMixture dim best\n", argv[0]);
+        return 2;
+    }
+    const std::string           type  = argv[2];
+    const std::vector<uint32_t> sizes = parseList(argv[3]), counts = parseList(argv[4]);
+    const uint32_t              M = atoi(argv[5]), K = atoi(argv[6]), D = atoi(argv[7]);
+    const bool                  readBest = atoi(argv[8]) != 0;
+    if (sizes.empty() || sizes.size() != counts.size())
+        return 2;
+    Rng                 rng{12345};
+    Mm::Gpu::MixtureSet ms(D);
+    std::vector<float>  v(D);
+    for (uint32_t k = 0; k < D; ++k)
+        v[k] = 0.5f + std::fabs(rng.normal());
+    ms.addCovariance(v);
+    std::vector<uint32_t> dens(K);
+    std::vector<double>   logw(K, std::log(1.0 / K));
+    for (uint32_t m = 0; m < M; ++m) {
+        for (uint32_t j = 0; j < K; ++j) {
+            for (uint32_t k = 0; k < D; ++k)
+                v[k] = rng.normal();
+            dens[j] = ms.addDensity(ms.addMean(v), 0);
+        }
+        ms.addMixture(dens, logw);
+    }
+    uint32_t maxF = 0;
+    for (uint32_t c : counts)
+        maxF = std::max(maxF, c);
+    std::vector<Mm::Gpu::FeatureVector> frames(maxF, Mm::Gpu::FeatureVector(D));
+    for (auto& f : frames)
+        for (auto& x : f)
+            x = rng.normal();
+    for (size_t i = 0; i < sizes.size(); ++i) {
+        const uint32_t         B = sizes[i], F = counts[i];
+        Mm::Gpu::Configuration cfg;
+        cfg.type       = type;
+        cfg.bufferSize = B;
+        std::string err;
+        auto        scorer = Mm::Gpu::createFeatureScorer(ms, cfg, &err);
+        if (!scorer) {
+            fprintf(stderr, "createFeatureScorer failed: %s\n", err.c_str());
+            return 3;
+        }
+        double   sink  = 0;
+        uint64_t sinkB = 0;
+        auto     consume = [&](const Mm::Gpu::Scorer& s) {
+            const uint32_t n   = s->nEmissions();
+            float          acc = 0;
+            for (uint32_t e = 0; e < n; ++e)
+                acc += s->score(e);
+            sink += acc;
+            if (readBest && s->hasBestDensity())
+                for (uint32_t e = 0; e < n; ++e)
+                    sinkB += s->bestDensity(e);
+        };
+        auto segment = [&](uint32_t t0, uint32_t t1) {
+            scorer->reset();
+            for (uint32_t t = t0; t < t1; ++t) {
+                if (scorer->isBuffered() && !scorer->bufferFilled())
+                    scorer->addFeature(frames[t]);
+                else
+                    consume(scorer->getScorer(frames[t]));
+            }
+            if (scorer->isBuffered())
+                while (!scorer->bufferEmpty())
+                    consume(scorer->flush());
+        };
+        segment(0, std::min<uint32_t>(F, std::max<uint32_t>(2 * B, 64)));  // warm-up
+        auto lc = [&]() -> uint32_t {
+            if (auto* b = dynamic_cast<Mm::Gpu::GpuBatchFeatureScorer*>(scorer.get()))
+                return b->nLaunches();
+            if (auto* u = dynamic_cast<Mm::Gpu::GpuFeatureScorer*>(scorer.get()))
+                return u->nLaunches();
+            return 0;
+        };
+        const uint32_t l0 = lc();
+        const auto     t0 = std::chrono::steady_clock::now();
+        segment(0, F);
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        printf("{\"type\": \"%s\", \"buffer_size\": %u, \"frames\": %u, \"seconds\": %.6f, \"frames_per_s\": %.1f, "
+               "\"launches\": %u, \"best\": %s, \"mixtures\": %u, \"densities\": %u, \"dim\": %u, \"checksum\": %.6e}\n",
+               type.c_str(), B, F, sec, F / sec, lc() - l0, readBest ? "true" : "false", M, M * K, D,
+               sink + double(sinkB));
+        fflush(stdout);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 2 && std::string(argv[1]) == "bench")
+        return benchMain(argc, argv);
     if (argc != 7 && argc != 8) {
         fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node]\n", argv[0]);
         return 2;
     }
     const std::string protocol = argc == 8 ? argv[7] : "recognizer";
-    if (protocol != "recognizer" && protocol != "node")
+    if (protocol != "recognizer" && protocol != "node" && protocol != "delayed")
         return 2;
+    const bool     delayed = protocol == "delayed";
+    const uint32_t kDelay  = 3;
+    std::deque<Mm::Gpu::Scorer> pending;
     const bool node = protocol == "node";
+    if (delayed && atoi(argv[5]) > 1)
+        return 2;  // a buffered context is valid only until the next getScorer() reuses its position
     const std::string modelPath(argv[1]);
     const std::string dump(".drvmodel");
     const bool        pms = !(modelPath.size() >= dump.size() &&
@@ -122,16 +264,29 @@ int main(int argc, char** argv) {
         if (!node)
             scorer->reset();  // Recognizer.cc:186
         const uint32_t t0 = F * seg / segments, t1 = F * (seg + 1) / segments;
+        auto take = [&](const Mm::Gpu::Scorer& s) {
+            if (!delayed)
+                return consume(s);
+            pending.push_back(s);
+            if (pending.size() > kDelay) {
+                consume(pending.front());
+                pending.pop_front();
+            }
+        };
         for (uint32_t t = t0; t < t1; ++t) {
             Mm::Gpu::FeatureVector f(frames.begin() + size_t(t) * D, frames.begin() + size_t(t + 1) * D);
             if (scorer->isBuffered() && !scorer->bufferFilled())  // Recognizer.cc:275-277, FeatureScorerNode.cc:131-134
                 scorer->addFeature(f);
             else
-                consume(scorer->getScorer(f));
+                take(scorer->getScorer(f));
         }
         if (scorer->isBuffered())  // Recognizer.cc:200-204, FeatureScorerNode.cc:148-154
             while (!scorer->bufferEmpty())
-                consume(scorer->flush());
+                take(scorer->flush());
+        while (!pending.empty()) {
+            consume(pending.front());
+            pending.pop_front();
+        }
         if (node) {  // FeatureScorerNode.cc:157-159
             scorer->finalize();
             scorer->reset();
@@ -140,6 +295,8 @@ int main(int argc, char** argv) {
     uint32_t launches = 0;
     if (auto* b = dynamic_cast<Mm::Gpu::GpuBatchFeatureScorer*>(scorer.get()))
         launches = b->nLaunches();
+    else if (auto* u = dynamic_cast<Mm::Gpu::GpuFeatureScorer*>(scorer.get()))
+        launches = u->nLaunches();
     FILE* fo = fopen(argv[3], "wb");
     const uint32_t oh[3] = {static_cast<uint32_t>(outS.size() / (M ? M : 1)), M, launches};
     fwrite(oh, sizeof(uint32_t), 3, fo);

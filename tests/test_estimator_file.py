@@ -134,7 +134,7 @@ def test_known_answer():
 
 
 @pytest.mark.parametrize("case", ["magic", "truncated", "density_index", "mixture_index", "zero_weight_mixture",
-                                  "empty_mixture", "covariance_weight", "size"])
+                                  "empty_mixture", "covariance_weight", "negative_covariance_weight", "size"])
 def test_reference_failures(case):
     D, means, covs, dens, mixtures = _tiny()
     if case == "density_index":
@@ -147,6 +147,8 @@ def test_reference_failures(case):
         mixtures = [[(0, 2.0), (1, 3.0)], []]
     elif case == "covariance_weight":
         covs = [(covs[0][0], 7.0)]
+    elif case == "negative_covariance_weight":  # verify(accumulator_.weight() > 0), GaussDensityEstimator.cc:216
+        covs = [(covs[0][0], -5.0)]
     elif case == "size":
         means = [(np.array([2.0, 4.0]), 2.0), means[1]]
     data = est.write_estimator_file(None, D, means, covs, dens, mixtures)

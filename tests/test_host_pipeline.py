@@ -109,3 +109,76 @@ def test_pinned_empty_roundtrip(built):
     a[:] = np.arange(15, dtype=np.uint32).reshape(3, 5)
     assert a.sum() == 105 and a.dtype == np.uint32 and a.shape == (3, 5)
     del a
+
+
+# ------------------------------------------------------------------------------------------------------------
+# gmm_score_host_ring / gmm_fetch_best_density: the BatchFeatureScorerBase ring in one call (wrapped or not),
+# best densities kept on the device until fetched
+
+
+def _ring_case(sc, ring, first, n, pinned, keep_best, frame_major=False):
+    m = sc.n_mixtures()
+    R = ring.shape[0]
+    mk = (lambda shape, dt: ra.pinned_empty(shape, dt)) if pinned else (lambda shape, dt: np.empty(shape, dt))
+    shape = (R + 2, m + 3) if frame_major else (m, R + 3)
+    out, best = mk(shape, np.float32), mk(shape, np.uint32)
+    out[:] = -7.0
+    best[:] = 123456
+    order = [(first + i) % R for i in range(n)]
+    ref_s, ref_b = _device_reference(sc, np.ascontiguousarray(ring[order]), True)
+    cid = sc.score_host_ring(ring, first, n, out, None if keep_best else best, keep_best=keep_best,
+                             frame_major=frame_major)
+    if keep_best:
+        assert (best == 123456).all()  # nothing copied yet
+        sc.fetch_best(cid, best)
+    pos = np.array(order, dtype=np.int64)
+    if frame_major:  # rows = ring positions, columns [0, m) = mixtures
+        got_s, got_b = out[pos, :m].T, best[pos, :m].T
+        rest = np.ones(shape, bool)
+        rest[pos, :m] = False
+    else:
+        got_s, got_b = out[:, pos], best[:, pos]
+        rest = np.ones(shape, bool)
+        rest[:, pos] = False
+    assert np.array_equal(np.ascontiguousarray(got_s).view(np.uint32), ref_s.view(np.uint32))
+    assert np.array_equal(got_b, ref_b)
+    assert (out[rest] == -7.0).all() and (best[rest] == 123456).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum"])
+@pytest.mark.parametrize("R,first,n", [(7, 5, 6), (7, 0, 7), (64, 63, 2), (64, 10, 30), (9000, 8000, 9000),
+                                       (20000, 3, 17000)])
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("keep_best", [False, True])
+@pytest.mark.parametrize("frame_major", [False, True])
+def test_ring_matches_device(gpu, model, kind, R, first, n, pinned, keep_best, frame_major):
+    """Small (one chunk) and pipelined (several chunks, the wrap inside a chunk) ring calls, pageable and pinned
+    tables, mixture- and frame-major: the ring positions equal gmm_score_device on the frames in ring order;
+    everything else is untouched."""
+    ring = ra.synthetic_frames(R, 33, seed=R + first)
+    sc = ra.Scorer(model, kind, max_frames=max(n, 64))
+    _ring_case(sc, ring, first, n, pinned, keep_best, frame_major)
+
+
+@pytest.mark.gpu
+def test_fetch_best_after_later_call_is_refused(gpu, model):
+    ring = ra.synthetic_frames(16, 33, seed=3)
+    sc = ra.Scorer(model, "SIMD-diagonal-maximum", max_frames=16)
+    m = sc.n_mixtures()
+    out, best = np.empty((m, 16), np.float32), np.empty((m, 16), np.uint32)
+    c1 = sc.score_host_ring(ring, 0, 8, out, keep_best=True)
+    c2 = sc.score_host_ring(ring, 8, 8, out, keep_best=True)
+    assert c2 > c1
+    with pytest.raises(ra.GmmError):
+        sc.fetch_best(c1, best)  # replaced on the device by c2
+    sc.fetch_best(c2, best)
+    with pytest.raises(ra.GmmError):  # keep_best with a best table, and a ring shorter than the run
+        sc.score_host_ring(ring, 0, 8, out, best, keep_best=True)
+    with pytest.raises(ra.GmmError):
+        sc.score_host_ring(ring[:4], 0, 8, out)
+    # batch types have no assignment: keep_best keeps nothing, fetching is refused
+    sb = ra.Scorer(model, "batch-diagonal-maximum-int", max_frames=16)
+    cid = sb.score_host_ring(ring, 3, 16, out, keep_best=True)
+    with pytest.raises(ra.GmmError):
+        sb.fetch_best(cid, best)

@@ -164,3 +164,23 @@ def test_protocol_model_from_estimator_file(gpu, tmp_path, kind):
         ref = oracle.OracleFloat(ms).score(frames)[0]
         assert (np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))).max() <= 1e-4
     del est
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum"])
+def test_delayed_consumer_unbuffered(gpu, tmp_path, kind):
+    """A consumer that reads each context only after 3 more frames were scored (RecognizerDelayHandler,
+    src/Speech/DelayedRecognizer.cc:65-135): scores come from the context's own page-locked slot, and its best
+    densities -- replaced on the device by the later frames -- come from scoring its frame again.  Every frame
+    but the last of each segment is scored twice (launches = 2F - segments)."""
+    ms = ra.synthetic_mixture_set(30, 9, 39, seed=52, weights="random")
+    frames = ra.synthetic_frames(29, 39, seed=53)
+    s, b, launches = _run(tmp_path, ms, frames, kind, 1, 2, protocol="delayed")
+    if kind == "SIMD-diagonal-maximum":
+        ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+        assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
+        assert np.array_equal(b.T, ref_b)
+    else:
+        ref_s, ref_b = oracle.OracleFloat(ms).score(frames)[:2]
+        assert (np.abs(s.T.astype(np.float64) - ref_s) / np.maximum(1, np.abs(ref_s))).max() <= 1e-4
+    assert launches == 2 * 29 - 2

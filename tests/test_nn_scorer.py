@@ -108,6 +108,13 @@ def test_nn_scorer_device_strides_and_errors(gpu):
     assert (b[:, 0] == 7.0).all() and (b[:, 131:] == 7.0).all()
     with pytest.raises(ra.GmmError):
         sc.score_host(ra.synthetic_frames(131, 39, seed=1))  # more than max_frames
+    # caller buffers the C-ABI would overrun: refused before the call
+    with pytest.raises(ValueError):
+        sc.score_host(x, out=np.empty((199, 160), np.float32))  # fewer rows than classes
+    with pytest.raises(ValueError):
+        sc.score_host(x, n_frames=131)  # more frames than rows given
+    with pytest.raises(ValueError):
+        sc.score_host(x[:, :38])  # narrower than the input dimension
     with pytest.raises(ra.GmmError):
         nn.NnScorer([(np.ones((4, 5), np.float32), None, "relu", 1.0),
                      (np.ones((6, 2), np.float32), None, "identity", 1.0)])  # 5 != 6
@@ -126,3 +133,28 @@ def test_nn_scorer_k_tile_counts(gpu, dims, frames):
     sc = nn.NnScorer(layers, max_frames=frames)
     s = sc.score_host(x)
     assert _err(s, nn_oracle.forward_bf16(layers, x).astype(np.float64)) <= 2e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["tanh", "elu", "sigmoid"])
+def test_nn_activations_near_zero(gpu, act):
+    """Hidden activations of tiny pre-activations (|z| ~ 1e-7 .. 1e-2).  tanh: the reference's std::tanh
+    (Math::FastMatrix::tanh, src/Math/FastMatrix.hh:776-780) is accurate there, so the device form must keep its
+    RELATIVE accuracy (bf16 keeps a small output to 2^-9 relative), which 1 - 2/(e + 1) alone loses by
+    cancellation.  elu: the reference itself forms exp(x) - 1 (FastMatrix.hh:1656-1665), whose absolute error
+    (~1e-7) the restatement and the device share: the absolute contract.  The top layer is the identity, so the
+    scores are -bf16(act(z)) element by element."""
+    rng = np.random.Generator(np.random.PCG64(11))
+    d_in, d_h = 64, 128
+    w = (rng.standard_normal((d_in, d_h)) * np.logspace(-7, -2, d_h)[None, :] / 8).astype(np.float32)
+    layers = [(w, None, act, 1.0), (np.eye(d_h, dtype=np.float32), None, "identity", 1.0)]
+    x = ra.synthetic_frames(40, d_in, seed=12)
+    sc = nn.NnScorer(layers, max_frames=40)
+    s = sc.score_host(x).astype(np.float64)
+    ref = nn_oracle.forward_bf16(layers, x).astype(np.float64)
+    if act == "tanh":
+        rel = np.abs(s - ref) / np.maximum(np.abs(ref), 1e-30)
+        print(f"{act}: max relative error {rel.max():.2e} for |ref| in [{np.abs(ref).min():.1e}, {np.abs(ref).max():.1e}]")
+        assert rel.max() <= 2 ** -6  # one bf16 ulp (<= 2^-7 relative) of the hidden output, either side, + series
+    else:
+        assert np.abs(s - ref).max() <= 1e-6 + 2 ** -7 * np.abs(ref).max()  # one bf16 ulp + exp(x) - 1
