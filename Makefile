@@ -8,9 +8,8 @@ HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 # quantized kernels: MFMA results straight into VGPRs (gfx950 has one unified register file),
 # so the v_lshl_add / v_min3 epilogue reads them without v_accvgpr_read copies.
 I8FLAGS   = -mllvm -amdgpu-mfma-vgpr-form
-# float kernels: default AGPR accumulators (measured faster for the f32 MFMA chains) and one
-# tile per loop step (GMM_F32_PAIR=0), see DESIGN.md "Measurements"
-F32FLAGS  = -DGMM_F32_PAIR=0
+# float kernels: default AGPR accumulators (measured faster for the f32 MFMA chains), see DESIGN.md "Measurements"
+F32FLAGS  =
 # split-f16 float kernel; no SLP packing: the diagonal-sum epilogue's adds were packed into v_pk_add_f32 /
 # v_pk_mul_f32, which issue slower than two scalar ops beside the MFMAs (A/B: -1.0 %; no packed ops elsewhere)
 SPLITFLAGS = -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize
@@ -132,13 +131,19 @@ oracle:
 # written under build/ for this check only; it pins no parity and nothing is linked.  Skipped where the
 # reference tree is absent (the GPU box).
 RASR_SRC ?= /root/reference/src
-check-integration: integration/rasr/Mm/GpuFeatureScorer.cc integration/rasr/Mm/GpuFeatureScorer.hh $(SRC)/host/GpuFeatureScorer.hh
+check-integration: integration/rasr/Mm/GpuFeatureScorer.cc integration/rasr/Mm/GpuFeatureScorer.hh $(SRC)/host/GpuFeatureScorer.hh \
+                   integration/rasr/Nn/GpuBatchFeatureScorer.cc integration/rasr/Nn/GpuBatchFeatureScorer.hh \
+                   integration/rasr/Nn/GpuBatchFeatureScorerNetwork.cc include/rasr_nn.h
 	@if [ -d "$(RASR_SRC)/Mm" ]; then \
 	    mkdir -p $(BUILD)/rasr_check && printf '#pragma once\n#define MODULE_MM_BATCH\n' > $(BUILD)/rasr_check/Modules.hh && \
 	    g++ -std=gnu++0x -fsyntax-only -funsigned-char -fno-exceptions -Wall -DPROC_x86_64 -DOS_linux \
 	        -DARCH_linux_x86_64 -D_GNU_SOURCE -I$(BUILD)/rasr_check -I$(RASR_SRC) -I/usr/include/libxml2 -Iinclude \
 	        -I$(SRC) integration/rasr/Mm/GpuFeatureScorer.cc && \
-	    echo "check-integration: adapter compiles against $(RASR_SRC)"; \
+	    g++ -std=gnu++0x -fsyntax-only -funsigned-char -fno-exceptions -Wall -DPROC_x86_64 -DOS_linux \
+	        -DARCH_linux_x86_64 -D_GNU_SOURCE -I$(BUILD)/rasr_check -I$(RASR_SRC) -I/usr/include/libxml2 \
+	        -Iinclude integration/rasr/Nn/GpuBatchFeatureScorer.cc && \
+	    echo "check-integration: adapters compile against $(RASR_SRC) (Mm; Nn protocol unit -- its network unit" \
+	         "includes Math/Blas.hh -> <cblas.h>, absent from this image, and is not checked)"; \
 	else echo "check-integration: $(RASR_SRC) absent, skipped"; fi
 
 clean:

@@ -70,9 +70,16 @@ uint32_t nn_scorer_input_dim(const nn_scorer* scorer);
  * Replaces BatchFeatureScorer::getScore's network_.forward(buffer_) (cc:148-171). */
 int nn_score_device(nn_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
                     float* scores, uint32_t score_stride, void* stream);
-/* Same with HOST buffers (copies in and out, synchronizes). */
+/* Same with HOST buffers (copies in and out, synchronizes; n_frames <= max_frames). */
 int nn_score_host(nn_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
                   float* scores, uint32_t score_stride);
+/* nn_score_host with flags.  NN_HOST_FRAME_MAJOR: scores are frame-major, scores[t * score_stride + e]
+ * (score_stride >= n_classes) -- the layout of the reference's output matrix, whose column t holds frame
+ * t's classes (Math::FastMatrix is column-major; BatchFeatureScorer::getScore reads at(e, position),
+ * BatchFeatureScorer.cc:148-171), so a context's score(e) calls read one contiguous row. */
+#define NN_HOST_FRAME_MAJOR 2u
+int nn_score_host_ex(nn_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
+                     float* scores, uint32_t score_stride, uint32_t flags);
 
 /* bench.py instrumentation, as gmm_scorer_set_timing / gmm_scorer_kernel_time: HIP events
  * around the layer GEMMs of every call; total GEMM time (ms) and call count since the last reset. */

@@ -26,18 +26,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef GMM_I8_LDS
 #define GMM_I8_LDS 1  // quantized kernel, one covariance: tiles staged through LDS (scoreI8Seg)
 #endif
-#ifndef GMM_F32_DEFER
-#define GMM_F32_DEFER 0  // float kernel: epilogue of tile t-1 issued with the MFMAs of tile t
-#endif
-#ifndef GMM_ABL_NO_EPI
-#define GMM_ABL_NO_EPI 0  // timing ablations (scripts/build_variants.sh); never set in the product build
-#endif
-#ifndef GMM_ABL_NO_LOAD
-#define GMM_ABL_NO_LOAD 0
-#endif
-#ifndef GMM_F32_PAIR
-#define GMM_F32_PAIR 1  // float kernel: two tiles per loop step
-#endif
 
 // ---------------------------------------------------------------------------
 // reference quantizer, device side (mirrors refRoundToInt / refQuantize in gmm_prepare.cc)

@@ -149,85 +149,21 @@ __global__ __launch_bounds__(256, GMM_F32_MIN_WAVES) void scoreF32(F32Args a) {
             }
 
         if constexpr (!MULTI) {
-            for (; GMM_F32_PAIR && t + 1 < tEnd; t += 2) {
-                f32x4 accA[NF], accB[NF];
-                chain(A0, accA);
-                loadTile(t + 2, A0);
-                chain(A1, accB);
-                loadTile(t + 3, A1);
-                const uint32_t tl = t - tBeg;
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        best[cb][r] = fminf(best[cb][r], fminf(key(accA[cb][r], tl), key(accB[cb][r], tl + 1)));
-            }
-#if GMM_F32_DEFER
-            // software pipeline: the min/argmin epilogue of tile t-1 is issued together with the MFMA
-            // chain of tile t (independent registers), so the VALU work fills MFMA issue gaps instead
-            // of stalling the chain; unrolled by two so the two accumulator sets never move.
-            const auto epi = [&](const f32x4(&acc)[NF], uint32_t tl) {
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        best[cb][r] = fminf(best[cb][r], key(acc[cb][r], tl));
-            };
-            const auto advance = [&]() {
-#pragma unroll
-                for (int s = 0; s < KS; ++s)
-                    A0[s] = A1[s];
-                loadTile(t + 2, A1);
-                ++t;
-            };
-            if (t < tEnd) {
-                f32x4    accP[NF], accQ[NF];
-                uint32_t tlP = t - tBeg, tlQ = 0;
-                chain(A0, accP);
-                advance();
-                for (;;) {
-                    if (t >= tEnd) {
-                        epi(accP, tlP);
-                        break;
-                    }
-                    tlQ = t - tBeg;
-                    chain(A0, accQ);
-                    epi(accP, tlP);
-                    advance();
-                    if (t >= tEnd) {
-                        epi(accQ, tlQ);
-                        break;
-                    }
-                    tlP = t - tBeg;
-                    chain(A0, accP);
-                    epi(accQ, tlQ);
-                    advance();
-                }
-            }
-#endif
-            for (; !GMM_F32_DEFER && t < tEnd;) {
+            // one tile per loop step (measured faster than two per step or a deferred epilogue,
+            // DESIGN.md section 4)
+            for (; t < tEnd;) {
                 f32x4 accA[NF];
                 chain(A0, accA);
                 const uint32_t tl = t - tBeg;
-#if GMM_ABL_NO_EPI  // ablation build only: keep every chain alive, drop the per-element epilogue
-                float keep = 0.0f;
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb)
-                    keep += accA[cb][0];
-                best[0][0] = fminf(best[0][0], key(keep, tl));
-#else
 #pragma unroll
                 for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         best[cb][r] = fminf(best[cb][r], key(accA[cb][r], tl));
-#endif
-#if !GMM_ABL_NO_LOAD  // ablation build only: reuse the first tile's operands
 #pragma unroll
                 for (int s = 0; s < KS; ++s)
                     A0[s] = A1[s];
                 loadTile(t + 2, A1);
-#endif
                 ++t;
             }
         }

@@ -36,21 +36,8 @@
 // minimum is a float key whose low tileBits mantissa bits hold the tile number.
 #include "gmm_device.hh"
 
-#ifndef GMM_SPLIT_DIAG
-#define GMM_SPLIT_DIAG 0  // timing diagnostics only (wrong results): 2 = keys without tags, 4 = no emit
-#endif
 #ifndef GMM_SPLIT_MIN_WAVES
 #define GMM_SPLIT_MIN_WAVES 1
-#endif
-#ifndef GMM_SPLIT_SLOTS
-#define GMM_SPLIT_SLOTS 4  // scoreSplit: running-minimum registers per column block (1, 2 or 4)
-#endif
-#ifndef GMM_SPLIT_PRIO
-#define GMM_SPLIT_PRIO 0  // A/B: 1 = s_setprio(1) over a pipeline step's MFMAs, 0 for the emit
-#endif
-#ifndef GMM_SPLIT_ORDER
-#define GMM_SPLIT_ORDER 0  // A/B: MFMA order of a step; 0 = tile A's chain then tile B's, 1 = the two tiles
-                           // alternate on one frame operand (B fragment shared by consecutive MFMAs)
 #endif
 #ifndef GMM_SPLIT_IL
 #define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
@@ -169,19 +156,14 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
 // lane l stores frame frame0 + l.  Straight-line code (no branch splits the basic block it is
 // scheduled into): uniform options are arithmetic, the frame bound is the buffer's num_records.
 // ---------------------------------------------------------------------------
-template <bool BEST, int S>
-__device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][S], uint32_t m,
+template <bool BEST>
+__device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][4], uint32_t m,
                                                  uint32_t frame0, int lane, uint32_t g, uint32_t kmask, int eOut,
                                                  float noneScore, float halfScale) {
     uint32_t k[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
-        if constexpr (S == 4)
-            k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
-        else if constexpr (S == 2)
-            k[cb] = min(best[cb][0], best[cb][1]);
-        else
-            k[cb] = best[cb][0];
+        k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
     // groups {g&1, g&1|2} of blocks (0,2) and (1,3): lanes < 32 keep blocks 0, 1, lanes >= 32 blocks 2, 3
     uint32_t w[2], wg[2];
 #pragma unroll
@@ -318,8 +300,9 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     const float noneScore = __fmul_rn(a.outScale, PRESEL ? a.backoff
                                                          : (a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f));
 
-    // running minima per column block; the key's tag holds (tile, slot r), so the 4 slots can share registers
-    constexpr int kSlots = PRESEL ? 4 : GMM_SPLIT_SLOTS;
+    // running minima per column block and accumulator slot (one register per slot measured fastest: 4.81 ms
+    // against 4.88 / 4.89 with the slots sharing 1 or 2 registers, profiles/r02/ab/ab_split_slots.txt)
+    constexpr int kSlots = 4;
     uint32_t      best[NF][kSlots];
     const auto    resetBest = [&]() {
 #pragma unroll
@@ -353,10 +336,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const uint32_t ka = (GMM_SPLIT_DIAG & 2) ? __float_as_uint(acc[0][cb][r])
-                                                         : (__float_as_uint(acc[0][cb][r]) & vmask) | tagA[r];
-                const uint32_t kb = (GMM_SPLIT_DIAG & 2) ? __float_as_uint(acc[1][cb][r])
-                                                         : (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
+                const uint32_t ka = (__float_as_uint(acc[0][cb][r]) & vmask) | tagA[r];
+                const uint32_t kb = (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
                 if constexpr (PRESEL) {
                     // tag | sign-extended mask byte (one v_or_b32_sdwa), made opaque so that the key stays
                     // one v_and_or_b32 (else the three ORs fold into v_or3 beside a separate v_and + v_bfe)
@@ -365,11 +346,6 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
                     asm("" : "+v"(ca), "+v"(cc));
                     best[cb][r] = umin3(best[cb][r], (__float_as_uint(acc[0][cb][r]) & vmask) | ca,
                                         (__float_as_uint(acc[1][cb][r]) & vmask) | cc);
-                }
-                else if constexpr (kSlots < 4) {
-                    // one v_min3 per update (the compiler would reassociate the chain into two-operand v_min)
-                    uint32_t& bs = best[cb][r % kSlots];
-                    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ka), "v"(kb));
                 }
                 else {
                     best[cb][r] = umin3(best[cb][r], ka, kb);
@@ -380,8 +356,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
     const auto emit = [&]() {
-        if (!(GMM_SPLIT_DIAG & 4) || m + 1 == m1)
-            emitMixtureSplit<BEST, kSlots>(a, best, m, frame0, lane, g, kmask, eOut, noneScore, 0.5f);
+        emitMixtureSplit<BEST>(a, best, m, frame0, lane, g, kmask, eOut, noneScore, 0.5f);
     };
     // after an emit at tile tNext: next mixture, and the empty ones that also end there (rare path)
     const auto advance = [&](uint32_t tNext) {
@@ -401,26 +376,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
                           const f32x4(&prev)[2][NF], uint32_t tPrev, const uint2& C0w, const uint2& C1w,
                           uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) {
-        if (GMM_SPLIT_PRIO)
-            __builtin_amdgcn_s_setprio(1);
-        if constexpr (GMM_SPLIT_ORDER == 1) {
-#pragma unroll
-            for (int cb = 0; cb < NF; ++cb) {
-                cur[0][cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                cur[1][cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            }
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-#pragma unroll
-                for (int cb = 0; cb < NF; ++cb) {
-                    cur[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[s], B[cb][s], cur[0][cb], 0, 0, 0);
-                    cur[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[s], B[cb][s], cur[1][cb], 0, 0, 0);
-                }
-        }
-        else {
-            chain(A0, cur[0]);
-            chain(A1, cur[1]);
-        }
+        chain(A0, cur[0]);
+        chain(A1, cur[1]);
         readSel(C0w, TTcur[0]);
         readSel(C1w, TTcur[1]);
         pairEpilogue(prev, tPrev - tBeg, TTprev);
@@ -434,8 +391,6 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     // the emit of the mixture that ended at tile tNext, if any (a separate block: with the emit inside
     // the interleaved one, the duplicated step needs more than 256 VGPRs)
     const auto finish = [&](uint32_t tNext) {
-        if (GMM_SPLIT_PRIO)
-            __builtin_amdgcn_s_setprio(0);
         if (tNext == tEnd) {
             emit();
             resetBest();

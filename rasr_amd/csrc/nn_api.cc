@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/rasr_nn.h"
+#include "gmm_kernels.hh"  // launchTransposeWords (gmm_kernels_layout.hip)
 #include "nn_kernels.hh"
 
 using namespace rasr_nn;
@@ -67,6 +68,11 @@ struct nn_scorer {
     bool               pending = false;
     double             totalMs = 0;
     uint32_t           nCalls  = 0;
+    // nn_score_host staging (lazily, for max_frames)
+    hipStream_t        hostStream = nullptr;
+    float*             dHostF = nullptr;  // [maxFrames][K]
+    float*             dHostS = nullptr;  // [M][maxFrames]
+    float*             dHostT = nullptr;  // [maxFrames][M] (frame-major)
 
     ~nn_scorer() {
         (void)hipSetDevice(device);
@@ -75,6 +81,10 @@ struct nn_scorer {
             (void)hipFree(l.dBias);
         }
         (void)hipFree(dX0);
+        for (float* p : {dHostF, dHostS, dHostT})
+            (void)hipFree(p);
+        if (hostStream)
+            (void)hipStreamDestroy(hostStream);
         for (auto* h : dH)
             (void)hipFree(h);
         if (ev0)
@@ -255,39 +265,62 @@ int nn_score_device(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_
 
 int nn_score_host(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
                   uint32_t scoreStride) {
+    return nn_score_host_ex(s, frames, nFrames, frameStride, scores, scoreStride, 0);
+}
+
+int nn_score_host_ex(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+                     uint32_t scoreStride, uint32_t flags) {
     if (!s || !frames || !scores)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    if ((flags & ~NN_HOST_FRAME_MAJOR) != 0)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "unknown flags");
     if (nFrames == 0)
         return GMM_OK;
+    if (nFrames > s->maxFrames)
+        return fail(GMM_ERR_CAPACITY, "n_frames exceeds max_frames");
+    const bool     frameMajor = (flags & NN_HOST_FRAME_MAJOR) != 0;
     const uint32_t K = s->layers[0].K, M = s->layers.back().M;
-    if (frameStride < K || scoreStride < nFrames)
+    if (frameStride < K || scoreStride < (frameMajor ? M : nFrames))
         return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frame/score stride");
     NN_HIP_CHECK(hipSetDevice(s->device));
-    // device staging: dense [nFrames][K] frames and [M][nFrames] scores; freed on every path
-    struct DeviceBuffers {
-        float* f = nullptr;
-        float* s = nullptr;
-        ~DeviceBuffers() {
-            (void)hipFree(f);
-            (void)hipFree(s);
-        }
-    } d;
-    NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d.f), static_cast<size_t>(nFrames) * K * sizeof(float)));
-    NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d.s), static_cast<size_t>(M) * nFrames * sizeof(float)));
-    // only the caller's K used floats per frame row are read, only its first nFrames columns per class row
-    // written (the rest of a strided caller buffer stays untouched, as with gmm_score_host)
-    NN_HIP_CHECK(hipMemcpy2D(d.f, static_cast<size_t>(K) * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
-                             static_cast<size_t>(K) * sizeof(float), nFrames, hipMemcpyHostToDevice));
-    const int rc = nn_score_device(s, d.f, nFrames, K, d.s, nFrames, nullptr);
-    if (rc != GMM_OK) {
-        (void)hipDeviceSynchronize();  // nothing of this call may still run when the buffers are freed
-        return rc;
+    // persistent staging (allocated once for max_frames) on the scorer's own stream: dense [F][K] frames,
+    // [M][F] scores and, frame-major, their transpose [F][M]
+    if (!s->hostStream) {
+        NN_HIP_CHECK(hipStreamCreateWithFlags(&s->hostStream, hipStreamNonBlocking));
+        NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostF), static_cast<size_t>(s->maxFrames) * K * sizeof(float)));
+        NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostS), static_cast<size_t>(s->maxFrames) * M * sizeof(float)));
     }
-    NN_HIP_CHECK(hipDeviceSynchronize());
-    NN_HIP_CHECK(hipMemcpy2D(scores, static_cast<size_t>(scoreStride) * sizeof(float), d.s,
-                             static_cast<size_t>(nFrames) * sizeof(float), static_cast<size_t>(nFrames) * sizeof(float), M,
-                             hipMemcpyDeviceToHost));
-    return GMM_OK;
+    if (frameMajor && !s->dHostT)
+        NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostT), static_cast<size_t>(s->maxFrames) * M * sizeof(float)));
+    // only the caller's K used floats per frame row are read; only the call's rows / columns of a strided caller
+    // table are written (the rest stays untouched, as with gmm_score_host)
+    int rc = GMM_OK;
+    auto run = [&]() -> int {
+        NN_HIP_CHECK(hipMemcpy2DAsync(s->dHostF, static_cast<size_t>(K) * sizeof(float), frames,
+                                      static_cast<size_t>(frameStride) * sizeof(float), static_cast<size_t>(K) * sizeof(float),
+                                      nFrames, hipMemcpyHostToDevice, s->hostStream));
+        int r = nn_score_device(s, s->dHostF, nFrames, K, s->dHostS, nFrames, s->hostStream);
+        if (r != GMM_OK)
+            return r;
+        if (frameMajor) {
+            NN_HIP_CHECK(rasr_gmm::launchTransposeWords(reinterpret_cast<const uint32_t*>(s->dHostS), M, nFrames, nFrames,
+                                                        reinterpret_cast<uint32_t*>(s->dHostT), M, s->hostStream));
+            NN_HIP_CHECK(hipMemcpy2DAsync(scores, static_cast<size_t>(scoreStride) * sizeof(float), s->dHostT,
+                                          static_cast<size_t>(M) * sizeof(float), static_cast<size_t>(M) * sizeof(float),
+                                          nFrames, hipMemcpyDeviceToHost, s->hostStream));
+        }
+        else
+            NN_HIP_CHECK(hipMemcpy2DAsync(scores, static_cast<size_t>(scoreStride) * sizeof(float), s->dHostS,
+                                          static_cast<size_t>(nFrames) * sizeof(float),
+                                          static_cast<size_t>(nFrames) * sizeof(float), M, hipMemcpyDeviceToHost,
+                                          s->hostStream));
+        NN_HIP_CHECK(hipStreamSynchronize(s->hostStream));
+        return GMM_OK;
+    };
+    rc = run();
+    if (rc != GMM_OK)
+        (void)hipStreamSynchronize(s->hostStream);  // nothing of this call may still run into the caller's buffers
+    return rc;
 }
 
 int nn_scorer_set_timing(nn_scorer* s, int enable) {

@@ -47,6 +47,9 @@ _PROTOTYPES = [
       ctypes.c_void_p]),
     ("nn_score_host", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]),
+    ("nn_score_host_ex", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+      ctypes.c_uint32]),
     ("nn_scorer_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("nn_scorer_kernel_time", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
@@ -143,21 +146,26 @@ class NnScorer:
                                        ctypes.c_void_p(scores.data_ptr()), int(scores.stride(0)),
                                        ctypes.c_void_p(s) if s else None), "nn_score_device")
 
-    def score_host(self, frames: np.ndarray, out: np.ndarray | None = None, n_frames: int | None = None) -> np.ndarray:
-        """nn_score_host.  frames: [F][>= input_dim] f32 rows (row stride = frames.shape[1]); out: optional
-        caller-kept [n_classes][>= F] table (row stride = out.shape[1]), only its first F columns are written."""
+    def score_host(self, frames: np.ndarray, out: np.ndarray | None = None, n_frames: int | None = None,
+                   frame_major: bool = False) -> np.ndarray:
+        """nn_score_host(_ex).  frames: [F][>= input_dim] f32 rows (row stride = frames.shape[1]); out: optional
+        caller-kept table, [>= n_classes][>= F] (row stride = out.shape[1]) of which only the first F columns are
+        written, or with frame_major [>= F][>= n_classes] of which the first F rows' first n_classes entries are."""
         frames = np.ascontiguousarray(frames, dtype=np.float32)
         if frames.ndim != 2 or frames.shape[1] < self.input_dim():
             raise ValueError("frames must be a 2-d f32 [n_frames][>= input_dim] array")
         f = frames.shape[0] if n_frames is None else int(n_frames)
         if not 0 <= f <= frames.shape[0]:
             raise ValueError(f"n_frames {f} outside [0, {frames.shape[0]}] (the rows of frames)")
-        scores = np.empty((self.n_classes(), f), dtype=np.float32) if out is None else out
+        c = self.n_classes()
+        shape = (f, c) if frame_major else (c, f)
+        scores = np.empty(shape, dtype=np.float32) if out is None else out
         if (scores.dtype != np.float32 or not scores.flags.c_contiguous or scores.ndim != 2
-                or scores.shape[0] < self.n_classes() or scores.shape[1] < f):
-            raise ValueError("out must be a C-contiguous f32 [>= n_classes][>= n_frames] array")
-        _check(self._l.nn_score_host(self._h, frames.ctypes.data_as(ctypes.c_void_p), f, frames.shape[1],
-                                     scores.ctypes.data_as(ctypes.c_void_p), scores.shape[1]), "nn_score_host")
+                or scores.shape[0] < shape[0] or scores.shape[1] < shape[1]):
+            raise ValueError(f"out must be a C-contiguous f32 [>= {shape[0]}][>= {shape[1]}] array")
+        _check(self._l.nn_score_host_ex(self._h, frames.ctypes.data_as(ctypes.c_void_p), f, frames.shape[1],
+                                        scores.ctypes.data_as(ctypes.c_void_p), scores.shape[1],
+                                        2 if frame_major else 0), "nn_score_host_ex")
         return scores
 
     def set_timing(self, enable: bool) -> None:

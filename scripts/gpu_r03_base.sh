@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 opening GPU session: parity tests, smoke and the default bench line on this round's first box.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r03_base
+OUT=gpurun_out/${RUN:-r03_base}
 mkdir -p $OUT
 export TMPDIR=/tmp
 step() {  # step <name> <timeout> <cmd...>

@@ -171,8 +171,9 @@ def test_protocol_model_from_estimator_file(gpu, tmp_path, kind):
 def test_delayed_consumer_unbuffered(gpu, tmp_path, kind):
     """A consumer that reads each context only after 3 more frames were scored (RecognizerDelayHandler,
     src/Speech/DelayedRecognizer.cc:65-135): scores come from the context's own page-locked slot, and its best
-    densities -- replaced on the device by the later frames -- come from scoring its frame again.  Every frame
-    but the last of each segment is scored twice (launches = 2F - segments)."""
+    densities -- replaced on the device by the later frames (or by the re-scoring of an older context, which
+    is itself a host call) -- come from scoring its frame again: every frame is scored twice (launches = 2F).
+    The buffered protocol of test_simd_protocol_bit_exact covers the copy-on-demand path."""
     ms = ra.synthetic_mixture_set(30, 9, 39, seed=52, weights="random")
     frames = ra.synthetic_frames(29, 39, seed=53)
     s, b, launches = _run(tmp_path, ms, frames, kind, 1, 2, protocol="delayed")
@@ -183,4 +184,4 @@ def test_delayed_consumer_unbuffered(gpu, tmp_path, kind):
     else:
         ref_s, ref_b = oracle.OracleFloat(ms).score(frames)[:2]
         assert (np.abs(s.T.astype(np.float64) - ref_s) / np.maximum(1, np.abs(ref_s))).max() <= 1e-4
-    assert launches == 2 * 29 - 2
+    assert launches == 2 * 29

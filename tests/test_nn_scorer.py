@@ -115,6 +115,13 @@ def test_nn_scorer_device_strides_and_errors(gpu):
         sc.score_host(x, n_frames=131)  # more frames than rows given
     with pytest.raises(ValueError):
         sc.score_host(x[:, :38])  # narrower than the input dimension
+    # frame-major host table (NN_HOST_FRAME_MAJOR): row t = frame t's classes, other entries untouched
+    fm = np.full((133, 205), 7.0, np.float32)
+    sc.score_host(x, out=fm, frame_major=True)
+    assert _err(fm[:130, :200].T, ref) <= 2e-3
+    assert (fm[130:] == 7.0).all() and (fm[:, 200:] == 7.0).all()
+    with pytest.raises(ValueError):
+        sc.score_host(x, out=np.empty((130, 199), np.float32), frame_major=True)
     with pytest.raises(ra.GmmError):
         nn.NnScorer([(np.ones((4, 5), np.float32), None, "relu", 1.0),
                      (np.ones((6, 2), np.float32), None, "identity", 1.0)])  # 5 != 6
