@@ -76,14 +76,17 @@ $(BUILD)/nn_api.o: $(SRC)/nn_api.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
-# identity of the device code (hash of the kernel sources and their flags): profiling summaries record it and
-# bench.py uses a summary only for the kernels it was measured on
-# the GMM scorer kernels the PMC summaries (profiles/pmc_*.json) measure: their sources and flags
-KERNEL_SRCS = $(SRC)/gmm_kernels_i8.hip $(SRC)/gmm_kernels_f32.hip $(SRC)/gmm_kernels_split.hip \
-              $(SRC)/gmm_device.hh $(SRC)/gmm_kernels.hh
-$(BUILD)/kernel_id.h: $(KERNEL_SRCS) Makefile
-	@mkdir -p $(BUILD)
-	@echo "#define GMM_KERNEL_ID \"$$( (cat $(KERNEL_SRCS); echo '$(HIPFLAGS) $(I8FLAGS) $(F32FLAGS) $(SPLITFLAGS)') | sha256sum | cut -c1-16)\"" > $@
+# identity of the device code: a hash of the gfx950 code objects of the GMM scorer kernels (the kernels the PMC
+# summaries profiles/pmc_*.json measure), so a summary stays matched to the ISA it was collected on -- a source
+# edit that leaves the code unchanged keeps the id, any code change gives a new one; bench.py uses a summary
+# only for the kernels it was measured on
+BUNDLER   = /opt/rocm/lib/llvm/bin/clang-offload-bundler
+KERNEL_OBJS = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o
+$(BUILD)/kernel_id.h: $(KERNEL_OBJS)
+	@for o in $(KERNEL_OBJS); do objcopy -O binary --only-section=.hip_fatbin $$o $$o.fatbin && \
+	     $(BUNDLER) --unbundle --type=o --input=$$o.fatbin --targets=hipv4-amdgcn-amd-amdhsa--$(ARCH) \
+	     --output=$$o.$(ARCH) || exit 1; done
+	@echo "#define GMM_KERNEL_ID \"$$(cat $(addsuffix .$(ARCH),$(KERNEL_OBJS)) | sha256sum | cut -c1-16)\"" > $@
 
 $(BUILD)/gmm_api.o: $(SRC)/gmm_api.cc $(HDRS) $(BUILD)/kernel_id.h
 	@mkdir -p $(BUILD)

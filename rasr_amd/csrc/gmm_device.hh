@@ -20,9 +20,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // re-reads (A/B, profiles/r02/ab/ab_store_nt.txt: -1.4 % fp32, -0.35 % SIMD)
 #define GMM_STORE_CPOL 2
 #endif
-#ifndef GMM_PERMLANE
-#define GMM_PERMLANE 1  // quantized kernel: reduce-scatter by v_permlane{32,16}_swap (else ds_bpermute)
-#endif
 #ifndef GMM_I8_LDS
 #define GMM_I8_LDS 1  // quantized kernel, one covariance: tiles staged through LDS (scoreI8Seg)
 #endif

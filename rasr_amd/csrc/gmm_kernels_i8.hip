@@ -29,37 +29,8 @@
 // This file: the quantized kernels (built with -mllvm -amdgpu-mfma-vgpr-form, see Makefile).
 #include "gmm_device.hh"
 
-#ifndef GMM_I8_DIAG
-#define GMM_I8_DIAG 0  // timing diagnostics only (wrong results): 2 = keys without the pack, 4 = emit only the
-                       // chunk's last mixture, 8 = f32 finalize instead of the f64 division, 16 = every step
-                       // reads the segment's first tiles (loop-invariant LDS reads)
-#endif
-#ifndef GMM_I8_FASTDIV
-#define GMM_I8_FASTDIV 1  // SIMD finalize: multiply by the double reciprocal, divide only next to an f32 midpoint
-#endif
-#ifndef GMM_I8_BUFSTORE
-#define GMM_I8_BUFSTORE 1  // emit: buffer stores bounded by num_records instead of a per-lane frame branch
-#endif
-#ifndef GMM_I8_EXTRA_LDS
-#define GMM_I8_EXTRA_LDS 0  // A/B only: dynamic LDS bytes added to scoreI8Seg's workgroup (limits workgroups per CU)
-#endif
-#ifndef GMM_I8_PRESEL_NIB
-#define GMM_I8_PRESEL_NIB 1  // preselection-batch-int: mask tables as one byte per (cluster, t) + expansion table (-20 %)
-#endif
 #ifndef GMM_I8_SLOTS
 #define GMM_I8_SLOTS 1  // scoreI8Seg: running-minimum registers per column block (1, 2 or 4; 1: -0.7 %)
-#endif
-#ifndef GMM_I8_MFMA32
-#define GMM_I8_MFMA32 0  // SIMD / batch-int, one covariance: 32x32x32 MFMA kernel scoreI8Seg32 (else scoreI8Seg)
-#endif
-#ifndef GMM_I8_MFMA32_CB
-#define GMM_I8_MFMA32_CB 4  // scoreI8Seg32: column blocks of 32 frames per wave (4 or 2)
-#endif
-#ifndef GMM_I8_MFMA32_MINS
-#define GMM_I8_MFMA32_MINS 8  // scoreI8Seg32: running minima per column block (8: one per candidate pair of a block)
-#endif
-#ifndef GMM_I8_MFMA32_INTERLEAVE
-#define GMM_I8_MFMA32_INTERLEAVE 0  // scoreI8Seg32: VALU per MFMA in a sched_group_barrier interleave (0 = off)
 #endif
 #ifndef GMM_I8_INTERLEAVE
 #define GMM_I8_INTERLEAVE 4  // VALU per MFMA in a sched_group_barrier interleave of the pair step (0 = off; 4: +2 %, 6: -4 %)
@@ -115,31 +86,23 @@ __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restri
                                                 uint32_t* __restrict__ bestOut, const int (&res)[NPL], uint32_t m,
                                                 uint32_t frame0, int lane, int ib, const int (&ssOut)[NPL]) {
     const uint32_t mo = m;
-#if GMM_I8_BUFSTORE
-    // frames >= nFrames fall outside num_records: the buffer stores drop them (no per-lane branch)
+    // frames >= nFrames fall outside num_records: the buffer stores drop them (no per-lane branch; -0.75 %
+    // against a per-lane frame test, profiles/r02)
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
                                                      static_cast<int>(a.nFrames * 4u), 0x00020000);
     const auto rb = __builtin_amdgcn_make_buffer_rsrc(bestOut ? bestOut + static_cast<size_t>(mo) * a.scoreStride
                                                               : nullptr,
                                                      (short)0, static_cast<int>(a.nFrames * 4u), 0x00020000);
-#endif
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
         const uint32_t f = frame0 + 64 * i + lane;
-#if !GMM_I8_BUFSTORE
-        if (f >= a.nFrames)
-            continue;
-#endif
         const int packed = res[i];
         // mixture without densities: minScore stays Core::Type<int>::max
         const bool     none = MAYBE_NONE && packed == INT_MAX;
         const int      q    = none ? INT_MAX : (packed >> ib) + ssOut[i];
         const uint32_t dns  = none ? 0xffffffffu : static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
         float score;
-        if (GMM_I8_DIAG & 8)
-            score = static_cast<float>(q) * a.s2;
-        else if (a.flavor == 0) {  // SimdFeatureScorer.cc:142: (f32)(0.5 * q / scalingSquared_) in double
-#if GMM_I8_FASTDIV
+        if (a.flavor == 0) {  // SimdFeatureScorer.cc:142: (f32)(0.5 * q / scalingSquared_) in double
             // y = q * 0.5 RN64(1/s2) is within 3 ulp of the exact quotient, so (f32)y equals (f32) of the
             // correctly rounded double quotient unless an f32 rounding midpoint (the 29 bits below f32
             // precision = 2^28) lies within 4 ulp of y: then the division itself (never, in practice:
@@ -150,25 +113,15 @@ __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restri
                 score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
             else
                 score = static_cast<float>(y);
-#else
-            score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
-#endif
         }
         else  // BatchFeatureScorer.cc:468: (f32)best / scale_
             score = __fdiv_rn(static_cast<float>(q), a.batchScale);
         // ScaledContextScorer::score (ScaledFeatureScorer.hh:62-64); a finite score times 1.0f is itself,
         // so the multiply is unconditional (a select on the uniform test costs more than the multiply)
         score = __fmul_rn(a.outScale, score);
-#if GMM_I8_BUFSTORE
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, f * 4u, 0, GMM_STORE_CPOL);
         if (bestOut)
             __builtin_amdgcn_raw_buffer_store_b32(dns, rb, f * 4u, 0, GMM_STORE_CPOL);
-#else
-        const size_t o = static_cast<size_t>(mo) * a.scoreStride + f;
-        scores[o]      = score;
-        if (bestOut)
-            bestOut[o] = dns;
-#endif
     }
 }
 
@@ -200,7 +153,6 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
     }
     int w[NF / 2];  // after the lane^32 step: column blocks cb with bit1 == (g >> 1)
     int res[NPL];   // after the lane^16 step: column block cb = g + 4 i
-#if GMM_PERMLANE
 #pragma unroll
     for (int p = 0; p < NF / 2; ++p) {
         const int c = (p & 1) | ((p >> 1) << 2);  // 0,1,4,5: bit1 clear
@@ -209,22 +161,6 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
 #pragma unroll
     for (int i = 0; i < NPL; ++i)
         res[i] = swapMin16(w[2 * i], w[2 * i + 1]);
-#else
-    const bool hi1 = (g >> 1) & 1, hi0 = g & 1;
-#pragma unroll
-    for (int p = 0; p < NF / 2; ++p) {
-        const int c    = (p & 1) | ((p >> 1) << 2);
-        const int send = hi1 ? v[c] : v[c ^ 2];
-        const int keep = hi1 ? v[c ^ 2] : v[c];
-        w[p]           = min(keep, __shfl_xor(send, 32));
-    }
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-        const int send = hi0 ? w[2 * i] : w[2 * i + 1];
-        const int keep = hi0 ? w[2 * i + 1] : w[2 * i];
-        res[i]         = min(keep, __shfl_xor(send, 16));
-    }
-#endif
 
     finalizeStoreI8<NPL, MAYBE_NONE>(a, scores, bestOut, res, m, frame0, lane, ib, ssOut);
 }
@@ -497,7 +433,6 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
 
     // preselection: this wave's 64-frame mask table [cluster][16] after the segment ring
     uint32_t laneSel = 0;  // byte offset of (wave table, column t = lane & 15)
-#if GMM_I8_PRESEL_NIB
     // compressed: one byte per (cluster, t) whose bit cb says "frame 16 cb + t did not select the cluster"
     // (4 KiB per wave instead of 16: 5 workgroups per CU instead of 2), expanded back to the 4-byte mask
     // word by a 16-entry table after the ring
@@ -523,16 +458,6 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         laneSel = tabOff + (static_cast<uint32_t>(lane) & 15u);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the table before the first segment's barrier
     }
-#else
-    if constexpr (PRESEL) {
-        const uint32_t words = a.nClusters * 16u;
-        const i32x4*   src   = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
-        i32x4*         dst   = reinterpret_cast<i32x4*>(lds + 2 * kSegBytes + kDummyBytes + static_cast<uint32_t>(wave) * words * 4u);
-        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u)
-            dst[i] = src[i];
-        laneSel = 2 * kSegBytes + kDummyBytes + (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
-    }
-#endif
     // a tile's row constants (the host biases them by 2^31 for PRESEL) and mask words of this lane's 4 rows,
     // from the tile's 64-byte row-constant block pRow and 32-byte cluster-offset block cRow
     const auto tileRows = [&](const int8_t* pRow, const int8_t* cRow, i32x4& P, uint32_t(&T)[4]) {
@@ -541,26 +466,17 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         if constexpr (PRESEL) {
             const uint2 cw = *reinterpret_cast<const uint2*>(cRow + g * 8);
             const int8_t* tb = lds + laneSel;
-#if GMM_I8_PRESEL_NIB
             // row offsets are cluster * 64 (the float kernel's word table); the byte table has 16 B per cluster
             const uint32_t* lut = reinterpret_cast<const uint32_t*>(lds + lutOff);
             T[0] = lut[*reinterpret_cast<const uint8_t*>(tb + ((cw.x & 0xffffu) >> 2))];
             T[1] = lut[*reinterpret_cast<const uint8_t*>(tb + (cw.x >> 18))];
             T[2] = lut[*reinterpret_cast<const uint8_t*>(tb + ((cw.y & 0xffffu) >> 2))];
             T[3] = lut[*reinterpret_cast<const uint8_t*>(tb + (cw.y >> 18))];
-#else
-            T[0] = *reinterpret_cast<const uint32_t*>(tb + (cw.x & 0xffffu));
-            T[1] = *reinterpret_cast<const uint32_t*>(tb + (cw.x >> 16));
-            T[2] = *reinterpret_cast<const uint32_t*>(tb + (cw.y & 0xffffu));
-            T[3] = *reinterpret_cast<const uint32_t*>(tb + (cw.y >> 16));
-#endif
         }
     };
 
     const uint32_t sh   = static_cast<uint32_t>(ib + 1);
     const auto     pack = [&](int acc, int p) {
-        if constexpr ((GMM_I8_DIAG & 2) != 0)
-            return acc;
         return static_cast<int>((static_cast<uint32_t>(acc) << sh) + static_cast<uint32_t>(p));
     };
     // candidate key: the packed value; PRESEL: biased, OR the mask byte of column block cb
@@ -602,8 +518,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, unb, mm, frame0, lane, g, ib, ssOut);
         }
         else {
-            if (!(GMM_I8_DIAG & 4) || mm + 1 == m1)
-                emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
+            emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, ib, ssOut);
         }
     };
     const std::true_type  kHot{};
@@ -631,7 +546,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         const uint32_t segEnd = min(segT0 + kSegTiles, T1);
         uint32_t       t      = segT0;
         while (t < segEnd) {
-            const uint32_t lt = (GMM_I8_DIAG & 16) ? 0u : t - segT0;
+            const uint32_t lt = t - segT0;
             // two tiles of the same mixture, or the last one beside the never-winning stand-in:
             // 2 NF independent MFMAs, one v_min3 per candidate pair
             const bool          two   = t + 1 < segEnd && t + 1 < tEnd;  // uniform
@@ -709,229 +624,6 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     }
 }
 
-
-// ---------------------------------------------------------------------------
-// quantized scorer, single covariance, on v_mfma_i32_32x32x32_i8 (GMM_I8_MFMA32)
-//
-// The kernel is bound by the SIMD's vector issue port, not by the matrix core: every MFMA holds the
-// port for 8 cycles whatever its shape (MI355X_MICROARCH.md, "vector-instruction ISSUE cost"), and
-// every candidate costs 1.5 three-source VOP3.  A 16x16x64 MFMA yields 4 candidates per lane for its
-// 8 held cycles; a 32x32x32 one yields 16 for half the K, i.e. 8 per 8 held cycles at K = 64: half the
-// hold per candidate.  Same LDS segment ring, same 16-row tiles and fragment data as scoreI8Seg: a
-// pair of 16-row tiles is one 32-row block, read with a per-lane remap (lane l: row l & 31 -> tile
-// t + ((l >> 4) & 1), k-block 2h + (l >> 5) of MFMA h), and the same 512 frames per workgroup (4
-// column blocks of 32 per wave).  Output layout of the 32x32 MFMA: lane l holds column (frame) l & 31,
-// register i row 8 (i >> 2) + 4 (l >> 5) + (i & 3); so lanes l and l ^ 32 share a frame and one
-// permlane32 swap-min stage leaves lane l with frame frame0 + 64 i + l, as in scoreI8Seg.
-// ---------------------------------------------------------------------------
-typedef int i32x16 __attribute__((ext_vector_type(16)));
-
-#ifndef GMM_I8_MFMA32_WAVES
-#define GMM_I8_MFMA32_WAVES 0  // scoreI8Seg32: waves per SIMD the register allocation aims at (0 = compiler's choice)
-#endif
-#if GMM_I8_MFMA32_WAVES
-#define GMM_I8_MFMA32_ATTR __attribute__((amdgpu_waves_per_eu(GMM_I8_MFMA32_WAVES, GMM_I8_MFMA32_WAVES)))
-#else
-#define GMM_I8_MFMA32_ATTR
-#endif
-template <int KS, int SEG, int CB>
-__global__ __launch_bounds__(256) GMM_I8_MFMA32_ATTR void scoreI8Seg32(I8Args a, const uint32_t* __restrict__ mixTileOff,
-                                                     float* __restrict__ scores, uint32_t* __restrict__ bestOut) {
-    // CB: column blocks of 32 frames per wave (4: 512 frames per workgroup, as scoreI8Seg; 2: 256 frames and
-    // half the registers, for 4 waves per SIMD -- the launcher doubles the frame-tile count)
-    static_assert(CB == 2 || CB == 4, "CB");
-    constexpr int      KH        = 2 * KS;                      // 32x32x32 MFMAs per block (K = 32 each)
-    constexpr int      NPL       = CB / 2;                      // results per lane per mixture
-    constexpr int      NB        = GMM_I8_MFMA32_MINS;          // running minima per column block
-    constexpr int      kSegTiles = SEG;
-    constexpr uint32_t kTileA    = KS * 1024;
-    constexpr uint32_t kSegA     = kSegTiles * kTileA;
-    constexpr uint32_t kSegBytes = kSegA + kSegTiles * 64;
-    constexpr int      kPieces   = kSegTiles * KS / 4;
-    constexpr int      kIssued   = kPieces + 1;
-    static_assert(kSegTiles * KS % 4 == 0, "segment pieces must split evenly over 4 waves");
-    static_assert(16 % (2 * NB) == 0 || NB == 8, "minima");
-    constexpr uint32_t kDummyBytes = kI8DummyTileBytes(KS, false);
-    __shared__ __attribute__((aligned(16))) int8_t lds[2 * kSegBytes + kDummyBytes];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int hl   = lane >> 5;  // lane half: k-block parity of the operands, row group of the result
-    uint32_t  chunk, ft;
-    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
-        return;  // uniform over the workgroup, before any barrier
-    const uint32_t frame0 = ft * (4u * CB * 32u) + static_cast<uint32_t>(wave) * (CB * 32u);
-    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
-    const int      ib = static_cast<int>(a.idxBits);
-    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
-    const uint32_t nSeg = (T1 - T0 + kSegTiles - 1) / kSegTiles;
-    const int8_t*  gA   = static_cast<const int8_t*>(a.tileA);
-    const int8_t*  gP   = static_cast<const int8_t*>(a.tileP);
-
-    const auto issueSeg = [&](uint32_t s) {
-        const uint32_t t0   = T0 + s * kSegTiles;
-        int8_t*        base = lds + (s & 1u) * kSegBytes;
-#pragma unroll
-        for (int i = 0; i < kPieces; ++i) {
-            const uint32_t piece = static_cast<uint32_t>(wave * kPieces + i);
-            __builtin_amdgcn_global_load_lds(gA + static_cast<size_t>(t0) * kTileA + piece * 1024u + lane * 16,
-                                             base + piece * 1024u, 16, 0, 0);
-        }
-        if (lane < kSegTiles)
-            __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * (kSegTiles * 16) + lane * 16,
-                                             base + kSegA + wave * (kSegTiles * 16), 16, 0, 0);
-    };
-    {
-        int8_t* const dummy = lds + 2 * kSegBytes;
-        for (uint32_t i = threadIdx.x; i < kDummyBytes / 4; i += 256u)
-            reinterpret_cast<uint32_t*>(dummy)[i] = (i >= kTileA / 4 && i < kTileA / 4 + 16) ? 0x7fffffffu : 0u;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    if (nSeg > 0)
-        issueSeg(0);
-    if (nSeg > 1)
-        issueSeg(1);
-
-    // frame operands: column block cb, MFMA h -> frame frame0 + 32 cb + (lane & 31), k-block 2h + hl
-    i32x4 B[CB][KH];
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-        const uint32_t f = frame0 + cb * 32 + (lane & 31);
-        const i32x4*   q = reinterpret_cast<const i32x4*>(a.frameQ + static_cast<size_t>(f) * (KS * 64)) + hl;
-#pragma unroll
-        for (int h = 0; h < KH; ++h)
-            B[cb][h] = q[2 * h];
-    }
-    int ssOut[NPL];
-#pragma unroll
-    for (int i = 0; i < NPL; ++i)
-        ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
-
-    // per-lane operand offset inside a tile (row lane & 15, k-block 2h + hl) and the row-constant offset
-    // of the lane's row group (rows 8j' + 4 hl + 0..3 of a 16-row tile, j' = 0, 1)
-    const uint32_t laneA   = static_cast<uint32_t>((hl * 16 + (lane & 15)) * 16);
-    const uint32_t upper   = (lane & 16) ? 0xffffffffu : 0u;  // lanes whose row lies in the second tile
-    const uint32_t laneP   = static_cast<uint32_t>(hl * 16);
-    const uint32_t sh      = static_cast<uint32_t>(ib + 1);
-    const auto     pack    = [&](int acc, int p) {
-        return static_cast<int>((static_cast<uint32_t>(acc) << sh) + static_cast<uint32_t>(p));
-    };
-    int        best[CB][NB];
-    const auto resetBest = [&]() {
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-            for (int r = 0; r < NB; ++r)
-                best[cb][r] = INT_MAX;
-    };
-    const auto emit = [&](uint32_t mm, auto hot) {
-        constexpr bool kMaybeNone = !decltype(hot)::value;
-        int            v[CB];
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-            int x = best[cb][0];
-#pragma unroll
-            for (int r = 1; r < NB; ++r)
-                x = min(x, best[cb][r]);
-            v[cb] = x;
-        }
-        int res[NPL];
-#pragma unroll
-        for (int i = 0; i < NPL; ++i) {
-#if GMM_PERMLANE
-            res[i] = swapMin32(v[2 * i], v[2 * i + 1]);
-#else
-            res[i] = min(hl ? v[2 * i + 1] : v[2 * i], __shfl_xor(hl ? v[2 * i] : v[2 * i + 1], 32));
-#endif
-        }
-        finalizeStoreI8<NPL, kMaybeNone>(a, scores, bestOut, res, mm, frame0, lane, ib, ssOut);
-    };
-    const std::true_type  kHot{};
-    const std::false_type kEmpty{};
-    resetBest();
-    uint32_t m    = m0;
-    uint32_t tEnd = mixTileOff[m0 + 1];
-    while (m < m1 && tEnd == T0) {
-        emit(m, kEmpty);
-        ++m;
-        tEnd = m < m1 ? mixTileOff[m + 1] : T1;
-    }
-
-    for (uint32_t s = 0; s < nSeg; ++s) {
-        if (s + 1 < nSeg)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kIssued) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        const int8_t*  base   = lds + (s & 1u) * kSegBytes;
-        const uint32_t segT0  = T0 + s * kSegTiles;
-        const uint32_t segEnd = min(segT0 + kSegTiles, T1);
-        uint32_t       t      = segT0;
-        while (t < segEnd) {
-            const uint32_t      lt    = t - segT0;
-            const bool          two   = t + 1 < segEnd && t + 1 < tEnd;  // uniform
-            const int8_t* const dummy = lds + 2 * kSegBytes;
-            const int8_t* const a0    = base + lt * kTileA;
-            const int8_t* const a1    = two ? a0 + kTileA : dummy;
-            const int8_t* const p0    = base + kSegA + lt * 64;
-            const int8_t* const p1    = two ? p0 + 64 : dummy + kTileA;
-            // lane's tile: t for rows 0..15 of the block, t+1 (or the stand-in) for rows 16..31
-            const uint32_t delta = static_cast<uint32_t>(a1 - a0);
-            const int8_t*  al    = a0 + (laneA + (delta & upper));
-            i32x4          A[KH];
-#pragma unroll
-            for (int h = 0; h < KH; ++h)
-                A[h] = *reinterpret_cast<const i32x4*>(al + (h >> 1) * 1024 + (h & 1) * 512);
-            // row constants of register group j = 0..3: rows 8 j + 4 hl + 0..3 of the 32-row block
-            i32x4 P[4];
-            P[0] = *reinterpret_cast<const i32x4*>(p0 + laneP);
-            P[1] = *reinterpret_cast<const i32x4*>(p0 + laneP + 32);
-            P[2] = *reinterpret_cast<const i32x4*>(p1 + laneP);
-            P[3] = *reinterpret_cast<const i32x4*>(p1 + laneP + 32);
-            i32x16 acc[CB];
-#pragma unroll
-            for (int cb = 0; cb < CB; ++cb) {
-                acc[cb] = i32x16{};
-#pragma unroll
-                for (int h = 0; h < KH; ++h)
-                    acc[cb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[h], B[cb][h], acc[cb], 0, 0, 0);
-            }
-#pragma unroll
-            for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-                for (int i = 0; i < 16; i += 2) {
-                    const int r = (i / 2) % NB;
-                    best[cb][r] = min(best[cb][r], min(pack(acc[cb][i], P[i >> 2][i & 3]),
-                                                       pack(acc[cb][i + 1], P[(i + 1) >> 2][(i + 1) & 3])));
-                }
-#if GMM_I8_MFMA32_INTERLEAVE
-#pragma unroll
-            for (int i = 0; i < CB * KH; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, GMM_I8_MFMA32_INTERLEAVE, 0);
-            }
-#endif
-            t += two ? 2u : 1u;
-            if (t == tEnd && m < m1) {
-                emit(m, kHot);
-                resetBest();
-                ++m;
-                tEnd = m < m1 ? mixTileOff[m + 1] : T1;
-                while (t == tEnd && m < m1) {
-                    emit(m, kEmpty);
-                    ++m;
-                    tEnd = m < m1 ? mixTileOff[m + 1] : T1;
-                }
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        if (s + 2 < nSeg)
-            issueSeg(s + 2);
-    }
-}
-
 }  // namespace dev
 
 using dev::prepareFramesI8;
@@ -952,7 +644,7 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
         if (a.presel) {  // preselection-batch-int: NF 4, 4-tile segments (ring + 4 mask tables < 80 KiB)
             constexpr int      kSeg  = 4;
             constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 32)) + kI8DummyTileBytes(KS, true);
-            const uint32_t     lds   = GMM_I8_PRESEL_NIB ? kRing + 64u + 4u * a.nClusters * 16u : kRing + 4u * a.nClusters * 64u;
+            const uint32_t     lds   = kRing + 64u + 4u * a.nClusters * 16u;
             static bool        attr  = false;
             if (!attr) {
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>),
@@ -964,19 +656,9 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
                                a.mixTileOff, a.scores, a.best);
             return;
         }
-#if GMM_I8_MFMA32
-        if constexpr (NF == 8) {
-            constexpr int kCb = GMM_I8_MFMA32_CB;
-            I8Args        b   = a;  // frame tiles of 4 x kCb x 32 frames (the host pads to 512)
-            b.nFrameTiles     = a.nFrameTiles * (4 / kCb);
-            hipLaunchKernelGGL((dev::scoreI8Seg32<KS, (KS == 1 ? dev::kSegTiles : 8), kCb>), dim3(grid * (4 / kCb)),
-                               dim3(256), 0, s, b, b.mixTileOff, b.scores, b.best);
-            return;
-        }
-#endif
         // 16-tile segments for one K step (34 KiB per workgroup, 4 per CU); 8 for two (also 34 KiB)
         hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS, false, (KS == 1 ? dev::kSegTiles : 8)>), dim3(grid), dim3(256),
-                           GMM_I8_EXTRA_LDS, s, a, a.mixTileOff, a.scores, a.best);
+                           0, s, a, a.mixTileOff, a.scores, a.best);
         return;
     }
 #endif

@@ -7,11 +7,8 @@
 
 namespace rasr_nn {
 
-#ifndef NN_GEMM_TILE
-#define NN_GEMM_TILE 256  // 256: nnGemm256 (8 waves, 128 KiB LDS); 128: nnGemm (4 waves), kept for A/B
-#endif
-constexpr uint32_t kNnTileM = NN_GEMM_TILE;  // output units per workgroup tile
-constexpr uint32_t kNnTileN = NN_GEMM_TILE;  // frames per workgroup tile
+constexpr uint32_t kNnTileM = 256;  // output units per workgroup tile (nnGemm8p: 8 waves, 128 KiB LDS)
+constexpr uint32_t kNnTileN = 256;  // frames per workgroup tile
 constexpr uint32_t kNnTileK = 64;            // K per pipeline stage
 
 // One layer: Out = act(A . B^T + bias) with A = W^T [Mpad][Kpad] (bf16 bits), B = layer input
