@@ -20,7 +20,7 @@ for p in "${PASSES[@]}"; do
   i=$((i+1))
   echo "=== pass $i: $p"
   timeout -k 10 300 rocprofv3 --pmc $p -d $OUT/p$i -o run --output-format csv -- \
-      python bench.py --mode $MODE --steps 2 --warmup 1 --launches 2 --cpu-baseline off --host-boundary off --no-extra-mode ${FRAMES:+--frames $FRAMES} > $OUT/p$i.log 2>&1
+      python bench.py --mode $MODE --steps 2 --warmup 1 --launches 2 --cpu-baseline off --host-boundary off --extras off --no-extra-mode ${FRAMES:+--frames $FRAMES} > $OUT/p$i.log 2>&1
   rc=$?
   echo "rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $OUT/p$i.log; exit $rc; fi
