@@ -149,8 +149,24 @@ check-integration: integration/rasr/Mm/GpuFeatureScorer.cc integration/rasr/Mm/G
 	         "includes Math/Blas.hh -> <cblas.h>, absent from this image, and is not checked)"; \
 	else echo "check-integration: $(RASR_SRC) absent, skipped"; fi
 
+# The RASR-side adapter LINKED and RUN on the CPU (test infrastructure): integration/rasr/Mm/GpuFeatureScorer.cc and
+# the real host classes (rasr_amd/csrc/host/GpuFeatureScorer.cc) inside test doubles of RASR's plugin machinery
+# (tests/rasr_harness/include, see its README), over an oracle-backed stand-in of the C-ABI; driven through the
+# factory, FeatureScorerScaling, the recognizer and the score-dump call sequences (tests/rasr_harness/harness.cc).
+HARNESS = $(BUILD)/tests/rasr_adapter_harness
+$(HARNESS): tests/rasr_harness/harness.cc tests/rasr_harness/gmm_standin.cc integration/rasr/Mm/GpuFeatureScorer.cc \
+            integration/rasr/Mm/GpuFeatureScorer.hh $(SRC)/host/GpuFeatureScorer.cc $(SRC)/host/GpuFeatureScorer.hh \
+            $(wildcard tests/rasr_harness/include/*/*.hh) oracle
+	@mkdir -p $(BUILD)/tests
+	g++ -std=c++17 -O1 -Wall -Wno-unused-variable -Itests/rasr_harness/include -Iinclude -I$(SRC) -o $@ \
+	    tests/rasr_harness/harness.cc tests/rasr_harness/gmm_standin.cc integration/rasr/Mm/GpuFeatureScorer.cc \
+	    $(SRC)/host/GpuFeatureScorer.cc -Loracle/_build -lgmm_oracle -Wl,-rpath,'$$ORIGIN/../../oracle/_build' -lm -pthread
+
+check-integration-link: $(HARNESS)
+	$(HARNESS)
+
 clean:
 	rm -rf $(BUILD) $(LIBDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean check-integration
+.PHONY: all oracle clean check-integration check-integration-link
