@@ -32,9 +32,6 @@
 #ifndef GMM_I8_SLOTS
 #define GMM_I8_SLOTS 1  // scoreI8Seg: running-minimum registers per column block (1, 2 or 4; 1: -0.7 %)
 #endif
-#ifndef GMM_I8_INTERLEAVE
-#define GMM_I8_INTERLEAVE 4  // VALU per MFMA in a sched_group_barrier interleave of the pair step (0 = off; 4: +2 %, 6: -4 %)
-#endif
 
 namespace rasr_gmm {
 namespace dev {
@@ -567,9 +564,8 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             uint32_t T0w[4] = {}, T1w[4] = {};
             tileRows(p0, c0, P0, T0w);
             tileRows(p1, c1, P1, T1w);
-            i32x4 accA[NF], accB[NF];
-#pragma unroll
-            for (int cb = 0; cb < NF; ++cb) {
+            i32x4      accA[NF], accB[NF];
+            const auto mfmas = [&](int cb) {
                 accA[cb] = i32x4{0, 0, 0, 0};
                 accB[cb] = i32x4{0, 0, 0, 0};
 #pragma unroll
@@ -577,9 +573,8 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                     accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
                     accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[ks], B[cb][ks], accB[cb], 0, 0, 0);
                 }
-            }
-#pragma unroll
-            for (int cb = 0; cb < NF; ++cb)
+            };
+            const auto epilogue = [&](int cb) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int ca = cand(accA[cb][r], P0[r], T0w[r], cb), cc = cand(accB[cb][r], P1[r], T1w[r], cb);
@@ -596,13 +591,22 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                     else
                         best[cb][r % kSlots] = min2(best[cb][r % kSlots], min2(ca, cc));
                 }
-#if GMM_I8_INTERLEAVE
+            };
+            // software pipeline over the column blocks: chunks {MFMAs of block cb, epilogue of block cb - 1}
+            // fenced by sched_barrier, so every epilogue reads results whose MFMA latency has passed (no
+            // hazard s_nop in the stream: 3 wait states per pair step instead of 99; -2.6 % at 32768 frames)
+            mfmas(0);
 #pragma unroll
-            for (int i = 0; i < 2 * NF * KS; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, GMM_I8_INTERLEAVE, 0);  // VALU
+            for (int cb = 1; cb < NF; ++cb) {
+                __builtin_amdgcn_sched_barrier(0);
+                mfmas(cb);
+                epilogue(cb - 1);
+                // inside the chunk: the MFMAs first, then the epilogue (the scheduler would lead with the VALU)
+                __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);
             }
-#endif
+            __builtin_amdgcn_sched_barrier(0);
+            epilogue(NF - 1);
             t += two ? 2u : 1u;
             // the mixture ending here, and further ones without tiles ending at the same point (rare)
             if (t == tEnd && m < m1) {
