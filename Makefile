@@ -17,13 +17,13 @@ HOSTFLAGS = -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 
 SRC       = rasr_amd/csrc
 HDRS      = include/rasr_gmm.h $(SRC)/gmm_presel.hh $(SRC)/gmm_prepare.hh $(SRC)/gmm_kernels.hh $(SRC)/gmm_device.hh \
-            $(SRC)/host/GpuFeatureScorer.hh $(SRC)/gmm_hostio.hh include/rasr_gmm_io.h include/rasr_nn.h $(SRC)/nn_kernels.hh
+            $(SRC)/host/GpuFeatureScorer.hh $(SRC)/gmm_hostio.hh include/rasr_gmm_io.h include/rasr_nn.h $(SRC)/nn_kernels.hh $(SRC)/gmm_shard.hh
 
 LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
             $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/MixtureSetEstimatorFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
             $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o $(BUILD)/gmm_kernels_shard.o $(BUILD)/gmm_hostio.o \
-            $(BUILD)/gmm_kernels_direct.o $(BUILD)/gmm_kernels_layout.o
+            $(BUILD)/gmm_kernels_direct.o $(BUILD)/gmm_kernels_layout.o $(BUILD)/gmm_shard.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 REFSORT   = $(BUILD)/tests/refsort_test
@@ -96,6 +96,11 @@ $(BUILD)/gmm_hostio.o: $(SRC)/gmm_hostio.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -pthread -c $< -o $@
 
+# density shard plan (gmm_scorer_create_sharded, gmm_density_shard_plan)
+$(BUILD)/gmm_shard.o: $(SRC)/gmm_shard.cc $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
+
 $(BUILD)/gmm_prepare.o: $(SRC)/gmm_prepare.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
@@ -114,7 +119,7 @@ $(BUILD)/MixtureSetEstimatorFile.o: $(SRC)/host/MixtureSetEstimatorFile.cc $(HDR
 
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz -pthread
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz -pthread -lrccl
 
 # host pin of the GPU std::sort replay (gmm_refsort.hh) against this image's std::sort
 $(REFSORT): tests/cpp/refsort_test.cc $(SRC)/gmm_refsort.hh

@@ -232,6 +232,40 @@ int gmm_shard_pack_keys(const float* scores, const uint32_t* best, const uint32_
 int gmm_shard_unpack_keys(const int64_t* keys, uint32_t rows, uint32_t n_frames, float* scores, uint32_t* best,
                           uint32_t stride, void* stream);
 
+/* The density shard plan over `world` GPUs (host-only): part r holds the mixture entries [E r / P, E (r+1) / P)
+ * of the CSR order.  shard_table (may be NULL) receives [world][5] = {entry_begin, entry_end, mixture_begin,
+ * mixture_end, first_offset} (first_offset: in-mixture index of the part's first entry of mixture_begin);
+ * split (may be NULL, room for world - 1) the mixtures held by more than one part, ascending; *n_split their
+ * number. */
+int gmm_density_shard_plan(const uint32_t* mixture_offsets, uint32_t n_mixtures, uint32_t world,
+                           uint32_t* shard_table, uint32_t* split, uint32_t* n_split);
+
+/* Density-sharded scorer for one process driving several GPUs (an RASR process whose model is split over
+ * the GPUs of a node): part r of the plan above is an ordinary scorer on devices[r]; a call scores every
+ * part on its own stream, combines the mixtures split between parts by a per-frame minimum over
+ * gmm_shard_pack_keys keys, and assembles the full [n_mixtures] table on devices[0].  The handle is a
+ * gmm_scorer: gmm_score_device (DEVICE pointers on devices[0]), gmm_score_host, gmm_score_host_ring (all
+ * flags), gmm_fetch_best_density and the accessors work on it.  Scorer types whose mixture score is the
+ * minimum over its densities only (SIMD-diagonal-maximum, diagonal-maximum, batch-diagonal-maximum-*):
+ * GMM_ERR_UNSUPPORTED otherwise.  Quantized types give the unsharded scorer's results bit for bit; the
+ * float types stay within their f32 contract (a part's split-f16 scaling follows its own densities).
+ * n_devices == 1 creates the unsharded scorer itself.  exchange: the per-frame reduce --
+ *   GMM_EXCHANGE_RCCL: an RCCL all-reduce(MIN) over the parts' keys (ncclCommInitAll over devices, one
+ *     stream per GPU; the devices must be distinct),
+ *   GMM_EXCHANGE_COPY: peer copies of the keys to devices[0] and a minimum kernel there (any devices,
+ *     repeats allowed: N parts on one GPU),
+ *   GMM_EXCHANGE_AUTO: RCCL when the devices are distinct, else COPY.
+ * config->mixture_begin / mixture_end must be 0 (the whole set is sharded). */
+#define GMM_EXCHANGE_AUTO 0
+#define GMM_EXCHANGE_RCCL 1
+#define GMM_EXCHANGE_COPY 2
+int gmm_scorer_create_sharded(const gmm_mixture_set* mixture_set, gmm_scorer_type type,
+                              const gmm_scorer_config* config, const int* devices, uint32_t n_devices,
+                              int exchange, gmm_scorer** out);
+/* Parts of a handle (1 for an unsharded one) and the exchange it resolved to (GMM_EXCHANGE_RCCL / _COPY;
+ * GMM_EXCHANGE_AUTO for an unsharded handle or a plan without split mixtures). */
+int gmm_scorer_shard_info(const gmm_scorer* scorer, uint32_t* n_parts, int* exchange);
+
 const char* gmm_last_error(void);
 const char* gmm_version(void);
 /* Identity of this build's device code (a hash of the kernel sources and compile flags); profiling

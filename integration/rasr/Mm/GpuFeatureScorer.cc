@@ -16,6 +16,9 @@ const Core::ParameterInt GpuFeatureScorer::paramBufferSize(
         "buffer-size", "frames scored per GPU launch (1: every frame on its own, unbuffered)", 4, 1);
 const Core::ParameterInt GpuFeatureScorer::paramDevice(
         "device", "HIP device of this process (one process per GPU)", 0, 0);
+const Core::ParameterIntVector GpuFeatureScorer::paramShardDevices(
+        "density-shard-devices", "HIP devices the model's densities are split over (empty: the whole model on device)",
+        ",", 0);
 const Core::ParameterFloat GpuFeatureScorer::paramMixtureWeightScale(
         "mixture-weight-scale", "scaling of the mixture weights", 1.0);
 const Core::ParameterFloat GpuFeatureScorer::paramGaussianScale(
@@ -131,6 +134,8 @@ GpuFeatureScorer::GpuFeatureScorer(const Core::Configuration& c, Core::Ref<const
     cfg.type               = scorerType;
     cfg.bufferSize         = paramBufferSize(c);
     cfg.device             = paramDevice(c);
+    for (s32 d : paramShardDevices(c))
+        cfg.shardDevices.push_back(d);
     cfg.mixtureWeightScale = paramMixtureWeightScale(c);
     cfg.gaussianScale      = paramGaussianScale(c);
     const Core::Configuration dc(c, "density-clustering");
@@ -145,7 +150,11 @@ GpuFeatureScorer::GpuFeatureScorer(const Core::Configuration& c, Core::Ref<const
     impl_ = Gpu::createFeatureScorer(ms, cfg, &err);
     if (!impl_)
         criticalError("GPU feature scorer: %s", err.c_str());
-    log("GPU feature scorer \"%s\" on device %d, buffer size %u", scorerType, cfg.device, cfg.bufferSize);
+    if (cfg.shardDevices.size() > 1)
+        log("GPU feature scorer \"%s\" density-sharded over %zu devices, buffer size %u", scorerType,
+            cfg.shardDevices.size(), cfg.bufferSize);
+    else
+        log("GPU feature scorer \"%s\" on device %d, buffer size %u", scorerType, cfg.device, cfg.bufferSize);
 }
 
 GpuFeatureScorer::~GpuFeatureScorer() {}

@@ -35,6 +35,9 @@ class GpuFeatureScorer : public AssigningFeatureScorer {
 public:
     static const Core::ParameterInt   paramBufferSize;          // "buffer-size" (BatchFeatureScorer.cc:27-28)
     static const Core::ParameterInt   paramDevice;              // "device": HIP device of this process
+    // "density-shard-devices": the model's densities split over these GPUs of the process (BASELINE config 4,
+    // gmm_scorer_create_sharded; RCCL all-reduce for the mixtures split between GPUs); empty: all on "device"
+    static const Core::ParameterIntVector paramShardDevices;
     static const Core::ParameterFloat paramMixtureWeightScale;  // GaussDiagonalMaximumFeatureScorer.cc:38-40
     static const Core::ParameterFloat paramGaussianScale;       // GaussDiagonalMaximumFeatureScorer.cc:42-44
     // the "density-clustering" sub-component of the preselection types (DensityClustering.cc:19-32)

@@ -90,6 +90,8 @@ class EstimatorConfig(ctypes.Structure):
 
 GMM_HOST_KEEP_BEST = 1
 GMM_HOST_FRAME_MAJOR = 2
+# gmm_scorer_create_sharded: the per-frame reduce of mixtures split between GPUs
+GMM_EXCHANGE = {"auto": 0, "rccl": 1, "copy": 2}
 
 # (name, restype, argtypes) for every function declared in include/rasr_gmm.h and rasr_gmm_io.h
 PROTOTYPES = [
@@ -134,6 +136,12 @@ PROTOTYPES = [
     ("gmm_shard_unpack_keys", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
       ctypes.c_void_p]),
+    ("gmm_density_shard_plan", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, _u32p]),
+    ("gmm_scorer_create_sharded", ctypes.c_int,
+     [ctypes.POINTER(MixtureSetDesc), ctypes.c_int, ctypes.POINTER(ScorerConfig), ctypes.c_void_p, ctypes.c_uint32,
+      ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("gmm_scorer_shard_info", ctypes.c_int, [ctypes.c_void_p, _u32p, ctypes.POINTER(ctypes.c_int)]),
     ("gmm_last_error", ctypes.c_char_p, []),
     # include/rasr_gmm_io.h
     ("gmm_mixture_set_read", ctypes.c_int,

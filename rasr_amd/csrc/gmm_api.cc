@@ -7,6 +7,7 @@
 // per-frame Context of the reference, SimdFeatureScorer.cc:22-35) and the
 // scorer.  No host synchronisation, no allocation on that path.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -22,6 +23,7 @@
 #include "gmm_kernels.hh"
 #include "gmm_prepare.hh"
 #include "gmm_presel.hh"
+#include "gmm_shard.hh"
 #include "kernel_id.h"  // build/kernel_id.h (Makefile): GMM_KERNEL_ID
 
 using namespace rasr_gmm;
@@ -80,6 +82,12 @@ void setLastError(const std::string& msg) {
     gLastError = msg;
 }
 }  // namespace rasr_gmm
+
+// gmm_scorer_create_sharded: the parts of a density-sharded handle (defined below)
+struct DensityGroup;
+struct DensityGroupDelete {
+    void operator()(DensityGroup* g) const;
+};
 
 struct gmm_scorer {
     gmm_scorer_type   type;
@@ -157,6 +165,9 @@ struct gmm_scorer {
     bool                                        timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     size_t                                      eventsUsed = 0;
+    // density-sharded handle (gmm_scorer_create_sharded): no model of its own; the parts score, this handle
+    // holds the full-table host staging on devices[0]
+    std::unique_ptr<DensityGroup, DensityGroupDelete> group;
 
     ~gmm_scorer() {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
@@ -273,6 +284,9 @@ struct TimedSpan {
     hipError_t end() { return s->timing ? hipEventRecord(e, stream) : hipSuccess; }
 };
 
+int groupScore(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
+               uint32_t* best, uint32_t scoreStride, hipStream_t stream);
+
 int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
               uint32_t* best, uint32_t scoreStride, hipStream_t stream) {
     if (nFrames == 0 || s->nMix == 0)
@@ -282,6 +296,8 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
     if (!frames || !scores || frameStride < s->D || scoreStride < nFrames)
         return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frames/scores/stride");
     GMM_HIP_CHECK(hipSetDevice(s->device));
+    if (s->group)
+        return groupScore(s, frames, nFrames, frameStride, scores, best, scoreStride, stream);
     const uint32_t fpb         = framesPerBlock(s);
     const uint32_t nFrameTiles = (nFrames + fpb - 1) / fpb;
     const uint32_t nPadCall    = nFrameTiles * fpb;  // rows the scorer reads
@@ -751,6 +767,191 @@ int scoreHost(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, u
     return rc;
 }
 
+
+// ---------------------------------------------------------------------------------------------------------
+// Density-sharded handles (gmm_scorer_create_sharded, BASELINE config 4 for a C / C++ caller): one process,
+// part r of the density shard plan (gmm_shard.hh) on devices[r].  A call, on the caller's stream S of
+// devices[0]:
+//   every part, on its own stream after S's start event: frames -> its device (peer copy; none on devices[0]),
+//     its sub-model scored into [nLocal][n], the split mixtures it holds packed into keys [nSplit][n]
+//     (INT64_MAX for the ones it does not hold), then
+//   the per-frame reduce of the keys: RCCL all-reduce(MIN) over all parts (ncclGroupStart/End, one comm per
+//     GPU), or peer copies of every part's keys to devices[0] and minShardKeys there;
+//   every part copies its whole mixtures (local rows [rowLo, rowHi)) into the full table's rows;
+//   S waits for every part, unpacks the split mixtures' keys into their rows.
+// The full table's other rows come straight from the parts: no all-gather (the caller reads one table).
+}  // namespace
+
+struct DensityPart {
+    gmm_scorer*  scorer = nullptr;  // sub-model (null: the part holds no mixture)
+    int          device = 0;
+    DensityShard shard;
+    uint32_t     nLocal = 0, rowLo = 0, rowHi = 0;             // rows [rowLo, rowHi): whole mixtures
+    std::vector<std::pair<uint32_t, uint32_t>> held;           // (split slot, local row)
+    uint32_t*    dHeldOffset = nullptr;                        // [held] in-mixture index of the row's first entry
+    hipStream_t  stream      = nullptr;
+    hipEvent_t   done        = nullptr;
+    float*       dFrames     = nullptr;  // [maxF][D] (parts not on devices[0])
+    float*       dScores     = nullptr;  // [nLocal][maxF]
+    uint32_t*    dBest       = nullptr;
+    int64_t*     dKeys       = nullptr;  // [nSplit][maxF]
+};
+
+struct DensityGroup {
+    std::vector<DensityPart> parts;
+    std::vector<uint32_t>    split;  // mixtures held by more than one part
+    int                      exchange = GMM_EXCHANGE_AUTO;
+    std::vector<ncclComm_t>  comms;
+    int                      lead     = 0;        // devices[0]
+    int64_t*                 dGather  = nullptr;  // COPY: [parts][nSplit][maxF] on the lead
+    int64_t*                 dReduced = nullptr;  // COPY: [nSplit][maxF]
+    hipEvent_t               start = nullptr, finish = nullptr;  // on the caller's stream (lead)
+    bool                     timing = false;
+
+    ~DensityGroup() {
+        for (DensityPart& p : parts) {
+            (void)hipSetDevice(p.device);
+            if (p.stream)
+                (void)hipStreamSynchronize(p.stream);
+        }
+        for (ncclComm_t c : comms)
+            if (c)
+                (void)ncclCommDestroy(c);
+        for (DensityPart& p : parts) {
+            (void)hipSetDevice(p.device);
+            for (void* q : {static_cast<void*>(p.dHeldOffset), static_cast<void*>(p.dFrames), static_cast<void*>(p.dScores),
+                            static_cast<void*>(p.dBest), static_cast<void*>(p.dKeys)})
+                if (q)
+                    (void)hipFree(q);
+            if (p.done)
+                (void)hipEventDestroy(p.done);
+            if (p.stream)
+                (void)hipStreamDestroy(p.stream);
+            if (p.scorer)
+                delete p.scorer;
+        }
+        (void)hipSetDevice(lead);
+        for (void* q : {static_cast<void*>(dGather), static_cast<void*>(dReduced)})
+            if (q)
+                (void)hipFree(q);
+        for (hipEvent_t ev : {start, finish})
+            if (ev)
+                (void)hipEventDestroy(ev);
+    }
+};
+
+namespace {
+
+#define GMM_NCCL_CHECK(expr)                                                                        \
+    do {                                                                                            \
+        ncclResult_t r_ = (expr);                                                                   \
+        if (r_ != ncclSuccess)                                                                      \
+            return fail(GMM_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_));        \
+    } while (0)
+
+int groupScore(gmm_scorer* s, const float* frames, uint32_t n, uint32_t frameStride, float* scores, uint32_t* best,
+               uint32_t scoreStride, hipStream_t stream) {
+    DensityGroup&  g        = *s->group;
+    const size_t   nS       = g.split.size(), keyN = nS * n, D = s->D;
+    const bool     withBest = best && hasAssignment(s);
+    const uint32_t P        = static_cast<uint32_t>(g.parts.size());
+    // the parts' buffers are free once the previous call's reads of them (on its stream) are done
+    GMM_HIP_CHECK(hipStreamWaitEvent(stream, g.finish, 0));
+    GMM_HIP_CHECK(hipEventRecord(g.start, stream));
+    for (DensityPart& p : g.parts) {
+        GMM_HIP_CHECK(hipSetDevice(p.device));
+        GMM_HIP_CHECK(hipStreamWaitEvent(p.stream, g.start, 0));
+        const float* f  = frames;
+        uint32_t     fs = frameStride;
+        if (p.dFrames) {
+            GMM_HIP_CHECK(hipMemcpy2DAsync(p.dFrames, D * sizeof(float), frames, static_cast<size_t>(frameStride) * sizeof(float),
+                                           D * sizeof(float), n, hipMemcpyDefault, p.stream));
+            f = p.dFrames, fs = s->D;
+        }
+        int rc;
+        if (p.scorer && (rc = scoreImpl(p.scorer, f, n, fs, p.dScores, withBest ? p.dBest : nullptr, n, p.stream)) != GMM_OK)
+            return rc;
+        if (nS) {
+            GMM_HIP_CHECK(launchFillShardKeys(p.dKeys, keyN, p.stream));
+            for (size_t h = 0; h < p.held.size(); ++h) {
+                const uint32_t slot = p.held[h].first, row = p.held[h].second;
+                GMM_HIP_CHECK(launchPackShardKeys(p.dScores + static_cast<size_t>(row) * n,
+                                                  withBest ? p.dBest + static_cast<size_t>(row) * n : nullptr,
+                                                  p.dHeldOffset + h, 1, n, n, p.dKeys + static_cast<size_t>(slot) * n,
+                                                  p.stream));
+            }
+        }
+    }
+    // the per-frame reduce of the split mixtures
+    const int64_t* reduced = nullptr;
+    if (nS && g.exchange == GMM_EXCHANGE_RCCL) {
+        GMM_NCCL_CHECK(ncclGroupStart());
+        for (uint32_t i = 0; i < P; ++i) {
+            DensityPart& p = g.parts[i];
+            GMM_HIP_CHECK(hipSetDevice(p.device));
+            GMM_NCCL_CHECK(ncclAllReduce(p.dKeys, p.dKeys, keyN, ncclInt64, ncclMin, g.comms[i], p.stream));
+        }
+        GMM_NCCL_CHECK(ncclGroupEnd());
+        reduced = g.parts[0].dKeys;  // part 0 is on the lead device
+    }
+    else if (nS) {
+        for (uint32_t i = 0; i < P; ++i) {
+            DensityPart& p = g.parts[i];
+            GMM_HIP_CHECK(hipSetDevice(p.device));
+            GMM_HIP_CHECK(hipMemcpyPeerAsync(g.dGather + i * keyN, g.lead, p.dKeys, p.device, keyN * sizeof(int64_t), p.stream));
+        }
+        reduced = g.dReduced;
+    }
+    // whole mixtures straight into the full table
+    for (DensityPart& p : g.parts) {
+        GMM_HIP_CHECK(hipSetDevice(p.device));
+        const size_t rows = p.rowHi - p.rowLo;
+        if (rows) {
+            const size_t dst = static_cast<size_t>(p.shard.mixBegin + p.rowLo) * scoreStride, src = static_cast<size_t>(p.rowLo) * n;
+            GMM_HIP_CHECK(hipMemcpy2DAsync(scores + dst, static_cast<size_t>(scoreStride) * 4, p.dScores + src, static_cast<size_t>(n) * 4,
+                                           static_cast<size_t>(n) * 4, rows, hipMemcpyDefault, p.stream));
+            if (withBest)
+                GMM_HIP_CHECK(hipMemcpy2DAsync(best + dst, static_cast<size_t>(scoreStride) * 4, p.dBest + src,
+                                               static_cast<size_t>(n) * 4, static_cast<size_t>(n) * 4, rows, hipMemcpyDefault,
+                                               p.stream));
+        }
+        GMM_HIP_CHECK(hipEventRecord(p.done, p.stream));
+    }
+    GMM_HIP_CHECK(hipSetDevice(g.lead));
+    for (DensityPart& p : g.parts)
+        GMM_HIP_CHECK(hipStreamWaitEvent(stream, p.done, 0));
+    if (nS && g.exchange != GMM_EXCHANGE_RCCL)
+        GMM_HIP_CHECK(launchMinShardKeys(g.dGather, P, keyN, g.dReduced, stream));
+    for (size_t i = 0; i < nS; ++i) {
+        const size_t row = static_cast<size_t>(g.split[i]) * scoreStride;
+        GMM_HIP_CHECK(launchUnpackShardKeys(reduced + i * n, 1, n, scores + row, withBest ? best + row : nullptr, scoreStride,
+                                            stream));
+    }
+    GMM_HIP_CHECK(hipEventRecord(g.finish, stream));
+    return GMM_OK;
+}
+
+// the handle whose prepared model answers model queries (quantization, launch info): a part's
+const gmm_scorer* modelOf(const gmm_scorer* s) {
+    if (s && s->group)
+        for (const DensityPart& p : s->group->parts)
+            if (p.scorer)
+                return p.scorer;
+    return s;
+}
+
+bool minReducible(gmm_scorer_type t) {
+    return t == GMM_SIMD_DIAGONAL_MAXIMUM || t == GMM_DIAGONAL_MAXIMUM || t == GMM_BATCH_DIAGONAL_MAXIMUM_FLOAT ||
+           t == GMM_BATCH_DIAGONAL_MAXIMUM_INT || t == GMM_BATCH_DIAGONAL_MAXIMUM_FAST;
+}
+
+}  // namespace
+
+void DensityGroupDelete::operator()(DensityGroup* g) const {
+    delete g;
+}
+
+namespace {
 }  // namespace
 
 extern "C" {
@@ -942,6 +1143,163 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     return GMM_OK;
 }
 
+int gmm_scorer_create_sharded(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scorer_config* config,
+                              const int* devices, uint32_t nDevices, int exchange, gmm_scorer** out) {
+    if (!ms || !out || !devices || nDevices == 0)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument or no devices");
+    *out = nullptr;
+    if (exchange != GMM_EXCHANGE_AUTO && exchange != GMM_EXCHANGE_RCCL && exchange != GMM_EXCHANGE_COPY)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "unknown exchange");
+    gmm_scorer_config cfg;
+    gmm_default_config(&cfg);
+    if (config)
+        cfg = *config;
+    if (!minReducible(type))
+        return fail(GMM_ERR_UNSUPPORTED, "density sharding combines split mixtures by a minimum: SIMD-diagonal-maximum, "
+                                         "diagonal-maximum and batch-diagonal-maximum-* only");
+    if (cfg.mixture_begin != 0 || cfg.mixture_end != 0)
+        return fail(GMM_ERR_UNSUPPORTED, "a density-sharded handle shards the whole mixture set (mixture_begin/end 0)");
+    if (!(cfg.score_scale > 0.0f))
+        return fail(GMM_ERR_UNSUPPORTED, "density sharding needs a positive score scale (the minimum commutes with it)");
+    if (cfg.max_frames == 0)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "max_frames must be > 0");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(GMM_ERR_DEVICE, "no HIP device available");
+    bool distinct = true;
+    for (uint32_t i = 0; i < nDevices; ++i) {
+        if (devices[i] < 0 || devices[i] >= ndev)
+            return fail(GMM_ERR_INVALID_ARGUMENT, "device index out of range");
+        for (uint32_t j = 0; j < i; ++j)
+            distinct = distinct && devices[j] != devices[i];
+    }
+    if (exchange == GMM_EXCHANGE_RCCL && !distinct)
+        return fail(GMM_ERR_UNSUPPORTED, "the RCCL exchange needs distinct devices (one rank per GPU); use GMM_EXCHANGE_COPY");
+    if (nDevices == 1)  // the unsharded scorer itself
+        return gmm_scorer_create(ms, type, &cfg, devices[0], out);
+
+    std::vector<DensityShard> plan;
+    std::string               err = planDensityShards(ms->mixture_offsets, ms->n_mixtures, nDevices, plan);
+    if (!err.empty())
+        return fail(GMM_ERR_INVALID_ARGUMENT, err);
+    std::unique_ptr<DensityGroup> g(new DensityGroup);
+    g->split = splitMixtures(plan);
+    g->lead  = devices[0];
+    g->exchange = g->split.empty() ? GMM_EXCHANGE_AUTO
+                                   : (exchange == GMM_EXCHANGE_AUTO ? (distinct ? GMM_EXCHANGE_RCCL : GMM_EXCHANGE_COPY) : exchange);
+    const size_t maxF = cfg.max_frames, nS = g->split.size();
+    const auto   isSplit = [&](uint32_t m) { return std::binary_search(g->split.begin(), g->split.end(), m); };
+    g->parts.resize(nDevices);
+    for (uint32_t r = 0; r < nDevices; ++r) {
+        DensityPart& p = g->parts[r];
+        p.device       = devices[r];
+        p.shard        = plan[r];
+        p.nLocal       = p.shard.mixEnd - p.shard.mixBegin;
+        GMM_HIP_CHECK(hipSetDevice(p.device));
+        GMM_HIP_CHECK(hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
+        GMM_HIP_CHECK(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
+        if (p.nLocal) {
+            // the part's sub-model: mixtures [mixBegin, mixEnd) cut to the entry range, the same densities, means
+            // and covariances (so model-global preparation -- the quantization scale -- is the unsharded one)
+            const uint32_t        mb = p.shard.mixBegin, eb = p.shard.entryBegin, ee = p.shard.entryEnd;
+            std::vector<uint32_t> lo(p.nLocal + 1);
+            for (uint32_t j = 0; j <= p.nLocal; ++j)
+                lo[j] = std::min(std::max(ms->mixture_offsets[mb + j], eb), ee);
+            lo[0] = std::max(eb, ms->mixture_offsets[mb]);
+            const uint32_t base = lo[0];
+            for (uint32_t& v : lo)
+                v -= base;
+            gmm_mixture_set sub     = *ms;
+            sub.n_mixtures          = p.nLocal;
+            sub.mixture_offsets     = lo.data();
+            sub.mixture_densities   = ms->mixture_densities + base;
+            sub.mixture_log_weights = ms->mixture_log_weights + base;
+            int rc = gmm_scorer_create(&sub, type, &cfg, p.device, &p.scorer);
+            if (rc != GMM_OK)
+                return rc;
+            GMM_HIP_CHECK(hipSetDevice(p.device));
+            GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p.dScores), p.nLocal * maxF * sizeof(float)));
+            GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p.dBest), p.nLocal * maxF * sizeof(uint32_t)));
+            p.rowLo = isSplit(mb) ? 1 : 0;
+            p.rowHi = isSplit(p.shard.mixEnd - 1) ? p.nLocal - 1 : p.nLocal;
+            p.rowHi = std::max(p.rowHi, p.rowLo);
+            std::vector<uint32_t> offsets;
+            for (uint32_t i = 0; i < nS; ++i)
+                if (g->split[i] >= mb && g->split[i] < p.shard.mixEnd) {
+                    p.held.emplace_back(i, g->split[i] - mb);
+                    offsets.push_back(g->split[i] == mb ? p.shard.firstOffset : 0);
+                }
+            if ((rc = upload(&p.dHeldOffset, offsets)) != GMM_OK)
+                return rc;
+        }
+        if (nS)
+            GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p.dKeys), nS * maxF * sizeof(int64_t)));
+        if (p.device != g->lead) {
+            GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p.dFrames), maxF * ms->dimension * sizeof(float)));
+            // xGMI peer access both ways: frames out of the lead, tables and keys into it
+            int can = 0;
+            GMM_HIP_CHECK(hipDeviceCanAccessPeer(&can, g->lead, p.device));
+            if (!can)
+                return fail(GMM_ERR_UNSUPPORTED, "devices without peer access");
+            for (int a : {g->lead, p.device}) {
+                GMM_HIP_CHECK(hipSetDevice(a));
+                const hipError_t e = hipDeviceEnablePeerAccess(a == g->lead ? p.device : g->lead, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    return fail(GMM_ERR_DEVICE, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+                (void)hipGetLastError();
+            }
+        }
+    }
+    if (g->exchange == GMM_EXCHANGE_RCCL) {
+        g->comms.assign(nDevices, nullptr);
+        GMM_NCCL_CHECK(ncclCommInitAll(g->comms.data(), static_cast<int>(nDevices), devices));
+    }
+    GMM_HIP_CHECK(hipSetDevice(g->lead));
+    if (g->exchange == GMM_EXCHANGE_COPY) {
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&g->dGather), nDevices * nS * maxF * sizeof(int64_t)));
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&g->dReduced), nS * maxF * sizeof(int64_t)));
+    }
+    GMM_HIP_CHECK(hipEventCreateWithFlags(&g->start, hipEventDisableTiming));
+    GMM_HIP_CHECK(hipEventCreateWithFlags(&g->finish, hipEventDisableTiming));
+
+    // the handle: no model of its own; the kernel layout of the parts (frame chunking) and the full table's size
+    const gmm_scorer* m = nullptr;
+    for (const DensityPart& p : g->parts)
+        if (p.scorer && !m)
+            m = p.scorer;
+    auto s        = std::make_unique<gmm_scorer>();
+    s->type       = type;
+    s->flavor     = m ? m->flavor : Flavor::Simd;
+    s->quantized  = m ? m->quantized : false;
+    s->split      = m ? m->split : false;
+    s->direct     = m ? m->direct : false;
+    s->splitRows  = m ? m->splitRows : 16;
+    s->device     = g->lead;
+    s->cfg        = cfg;
+    s->D          = ms->dimension;
+    s->C          = ms->n_covariances;
+    s->nMix       = ms->n_mixtures;
+    s->nFramesPad = (cfg.max_frames + kFramePadQuantum - 1) / kFramePadQuantum * kFramePadQuantum;
+    if (!m) {
+        bool q = false, ok = false;
+        s->flavor    = flavorOf(type, &q, &ok);
+        s->quantized = q;
+    }
+    s->group.reset(g.release());
+    *out = s.release();
+    return GMM_OK;
+}
+
+int gmm_scorer_shard_info(const gmm_scorer* s, uint32_t* nParts, int* exchange) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    if (nParts)
+        *nParts = s->group ? static_cast<uint32_t>(s->group->parts.size()) : 1u;
+    if (exchange)
+        *exchange = s->group ? s->group->exchange : GMM_EXCHANGE_AUTO;
+    return GMM_OK;
+}
+
 int gmm_scorer_destroy(gmm_scorer* s) {
     if (!s)
         return GMM_OK;
@@ -1028,6 +1386,7 @@ int gmm_host_free(void* ptr) {
 int gmm_scorer_quantization(const gmm_scorer* s, float* scaling, float* invQ) {
     if (!s)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    s = modelOf(s);  // a sharded handle: its parts share the model-global quantization scale
     if (!s->quantized)
         return fail(GMM_ERR_UNSUPPORTED, "scorer type is not quantized");
     if (scaling)
@@ -1040,6 +1399,7 @@ int gmm_scorer_quantization(const gmm_scorer* s, float* scaling, float* invQ) {
 int gmm_scorer_multiply_and_quantize(const gmm_scorer* s, const float* feature, uint8_t* out) {
     if (!s || !feature || !out)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    s = modelOf(s);
     if (!s->quantized)
         return fail(GMM_ERR_UNSUPPORTED, "scorer type is not quantized");
     const uint32_t Dp = s->paddedDimension;
@@ -1081,6 +1441,7 @@ int gmm_prepare_quantized_host(const gmm_mixture_set* ms, gmm_scorer_type type, 
 int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLaunches, const char** name) {
     if (!s)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    s = modelOf(s);  // a sharded handle: per part
     (void)nFrames;
     if (nLaunches)
         *nLaunches = s->presel ? 3 : 2;
@@ -1096,12 +1457,34 @@ int gmm_scorer_set_timing(gmm_scorer* s, int enable) {
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
     s->timing     = enable != 0;
     s->eventsUsed = 0;
+    if (s->group)  // sharded: every part times its own kernels
+        for (DensityPart& p : s->group->parts)
+            if (p.scorer)
+                gmm_scorer_set_timing(p.scorer, enable);
     return GMM_OK;
 }
 
 int gmm_scorer_kernel_time(gmm_scorer* s, double* totalMs, uint32_t* nLaunches, int reset) {
     if (!s)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    if (s->group) {  // sharded: the parts run concurrently -- the slowest part's total, its launch count
+        double   worst = 0;
+        uint32_t n     = 0;
+        for (DensityPart& p : s->group->parts) {
+            double   t = 0;
+            uint32_t k = 0;
+            int      rc;
+            if (p.scorer && (rc = gmm_scorer_kernel_time(p.scorer, &t, &k, reset)) != GMM_OK)
+                return rc;
+            if (p.scorer && (t > worst || n == 0))
+                worst = t, n = k;
+        }
+        if (totalMs)
+            *totalMs = worst;
+        if (nLaunches)
+            *nLaunches = n;
+        return GMM_OK;
+    }
     GMM_HIP_CHECK(hipSetDevice(s->device));
     double total = 0;
     for (size_t i = 0; i < s->eventsUsed; ++i) {

@@ -159,6 +159,8 @@ hipError_t launchPackShardKeys(const float* scores, const uint32_t* best, const 
                                uint32_t nFrames, uint32_t stride, int64_t* keys, hipStream_t stream);
 hipError_t launchUnpackShardKeys(const int64_t* keys, uint32_t rows, uint32_t nFrames, float* scores, uint32_t* best,
                                  uint32_t stride, hipStream_t stream);
+hipError_t launchFillShardKeys(int64_t* keys, size_t n, hipStream_t stream);  // keys[i] = INT64_MAX
+hipError_t launchMinShardKeys(const int64_t* slots, uint32_t nSlots, size_t n, int64_t* out, hipStream_t stream);
 
 // frame-major host tables (gmm_kernels_layout.hip): dst[c * dstPitch + r] = src[r * srcPitch + c], 32-bit words
 hipError_t launchTransposeWords(const uint32_t* src, uint32_t rows, uint32_t cols, uint32_t srcPitch, uint32_t* dst,

@@ -58,6 +58,25 @@ __global__ __launch_bounds__(256) void unpackShardKeys(const int64_t* __restrict
         best[o] = static_cast<uint32_t>(k);
 }
 
+// identity of the per-frame reduce: the keys of split mixtures a GPU holds no part of
+__global__ __launch_bounds__(256) void fillShardKeys(int64_t* __restrict__ keys, size_t n) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n)
+        keys[i] = INT64_MAX;
+}
+
+// the per-frame reduce of the copy exchange: out[i] = min over the slots' keys (slot j at slots + j * n)
+__global__ __launch_bounds__(256) void minShardKeys(const int64_t* __restrict__ slots, uint32_t nSlots, size_t n,
+                                                    int64_t* __restrict__ out) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    int64_t k = slots[i];
+    for (uint32_t j = 1; j < nSlots; ++j)
+        k = min(k, slots[j * n + i]);
+    out[i] = k;
+}
+
 }  // namespace dev
 
 hipError_t launchPackShardKeys(const float* scores, const uint32_t* best, const uint32_t* bestOffset, uint32_t rows,
@@ -77,6 +96,21 @@ hipError_t launchUnpackShardKeys(const int64_t* keys, uint32_t rows, uint32_t nF
         return hipSuccess;
     hipLaunchKernelGGL(dev::unpackShardKeys, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, stream, keys,
                        rows, nFrames, scores, best, stride);
+    return hipGetLastError();
+}
+
+hipError_t launchFillShardKeys(int64_t* keys, size_t n, hipStream_t stream) {
+    if (n == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(dev::fillShardKeys, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, stream, keys, n);
+    return hipGetLastError();
+}
+
+hipError_t launchMinShardKeys(const int64_t* slots, uint32_t nSlots, size_t n, int64_t* out, hipStream_t stream) {
+    if (n == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(dev::minShardKeys, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, stream, slots,
+                       nSlots, n, out);
     return hipGetLastError();
 }
 

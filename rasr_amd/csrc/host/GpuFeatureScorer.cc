@@ -150,7 +150,12 @@ bool FeatureScorer::init(const MixtureSet& ms, const Configuration& c, uint32_t 
     cfg.clustering_iterations = c.clusteringIterations;
     cfg.backoff_score         = c.backoffScore;
     const gmm_mixture_set d  = ms.descriptor();
-    if (gmm_scorer_create(&d, t, &cfg, c.device, &handle_) != GMM_OK) {
+    const int rc = c.shardDevices.size() > 1
+                           ? gmm_scorer_create_sharded(&d, t, &cfg, c.shardDevices.data(),
+                                                       static_cast<uint32_t>(c.shardDevices.size()), GMM_EXCHANGE_AUTO,
+                                                       &handle_)
+                           : gmm_scorer_create(&d, t, &cfg, c.device, &handle_);
+    if (rc != GMM_OK) {
         if (error)
             *error = gmm_last_error();
         handle_ = nullptr;

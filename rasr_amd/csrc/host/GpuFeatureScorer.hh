@@ -118,6 +118,9 @@ struct Configuration {
     float       gaussianScale      = 1.0f;  // "gaussian-scale" (GDMFS.cc:42-44)
     float       scale              = 1.0f;  // FeatureScorerScaling scale (ScaledFeatureScorer.hh:62-64)
     int         device             = 0;
+    // more than one: the density-sharded scorer over these devices (gmm_scorer_create_sharded, exchange
+    // GMM_EXCHANGE_AUTO: RCCL for distinct devices); device is then ignored
+    std::vector<int> shardDevices;
     // "density-clustering" of the preselection scorers (DensityClustering.cc:19-32)
     uint32_t clusters             = 256;
     uint32_t selectClusters       = 32;

@@ -26,14 +26,16 @@ def default_config() -> _capi.ScorerConfig:
 
 
 class Scorer:
-    """One prepared model resident on one GPU (gmm_scorer_create)."""
+    """One prepared model resident on one GPU (gmm_scorer_create), or -- with `devices` -- the density-sharded
+    handle over several (gmm_scorer_create_sharded: part r of the density shard plan on devices[r], the full
+    table assembled on devices[0], `exchange` "auto" / "rccl" / "copy" for the per-frame reduce)."""
 
     def __init__(self, mixture_set: MixtureSet, scorer_type="SIMD-diagonal-maximum", max_frames: int = 4096,
                  device: int = 0, mixture_weight_scale: float = 1.0, gaussian_scale: float = 1.0,
                  score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None, native_f32: bool = False,
                  split_tile16: bool = False, split_tile32: bool = False, clusters: int = 256,
                  select_clusters: int = 32, clustering_iterations: int = 5, backoff_score: float = 40000.0,
-                 reference_order: bool = False):
+                 reference_order: bool = False, devices=None, exchange: str = "auto"):
         self._lib = _capi.load_library()
         self.mixture_set = mixture_set
         self.type = _type_id(scorer_type)
@@ -60,10 +62,23 @@ class Scorer:
         self.max_frames = int(max_frames)
         self._desc = mixture_set.desc()
         h = ctypes.c_void_p()
-        _capi.check(self._lib.gmm_scorer_create(ctypes.byref(self._desc), self.type, ctypes.byref(cfg), int(device),
-                                                ctypes.byref(h)), "gmm_scorer_create")
+        if devices is None:
+            _capi.check(self._lib.gmm_scorer_create(ctypes.byref(self._desc), self.type, ctypes.byref(cfg),
+                                                    int(device), ctypes.byref(h)), "gmm_scorer_create")
+        else:
+            devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            _capi.check(self._lib.gmm_scorer_create_sharded(ctypes.byref(self._desc), self.type, ctypes.byref(cfg),
+                                                            devs, len(devices), _capi.GMM_EXCHANGE[exchange],
+                                                            ctypes.byref(h)), "gmm_scorer_create_sharded")
+            device = int(devices[0])
         self._h = h
         self.device = device
+
+    def shard_info(self) -> tuple[int, str]:
+        """(parts, exchange) of the handle: (1, "auto") unsharded."""
+        n, x = ctypes.c_uint32(), ctypes.c_int()
+        _capi.check(self._lib.gmm_scorer_shard_info(self._h, ctypes.byref(n), ctypes.byref(x)), "gmm_scorer_shard_info")
+        return n.value, {v: k for k, v in _capi.GMM_EXCHANGE.items()}[x.value]
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

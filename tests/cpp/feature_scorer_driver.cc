@@ -243,6 +243,10 @@ int main(int argc, char** argv) {
     Mm::Gpu::Configuration cfg;
     cfg.type       = argv[4];
     cfg.bufferSize = static_cast<uint32_t>(atoi(argv[5]));
+    // RASR_DRIVER_SHARD_DEVICES="0,0,0": the density-sharded scorer ("density-shard-devices" of the adapter)
+    if (const char* sd = std::getenv("RASR_DRIVER_SHARD_DEVICES"))
+        for (uint32_t d : parseList(sd))
+            cfg.shardDevices.push_back(static_cast<int>(d));
     std::string                             err;
     std::unique_ptr<Mm::Gpu::FeatureScorer> scorer = Mm::Gpu::createFeatureScorer(ms, cfg, &err);
     if (!scorer) {

@@ -102,6 +102,18 @@ int gmm_scorer_create(const gmm_mixture_set* m, gmm_scorer_type type, const gmm_
     return GMM_OK;
 }
 
+// the sharded handle: the stand-in records the device list it was asked for (the harness checks that the
+// adapter's "density-shard-devices" reaches it) and scores the whole model (sharding does not change results)
+std::vector<int> gStandinShardDevices;
+
+int gmm_scorer_create_sharded(const gmm_mixture_set* m, gmm_scorer_type type, const gmm_scorer_config* cfg,
+                              const int* devices, uint32_t n, int exchange, gmm_scorer** out) {
+    if (!devices || n == 0 || exchange != GMM_EXCHANGE_AUTO)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "stand-in: devices / exchange");
+    gStandinShardDevices.assign(devices, devices + n);
+    return gmm_scorer_create(m, type, cfg, devices[0], out);
+}
+
 int gmm_scorer_destroy(gmm_scorer* s) {
     delete s;
     return GMM_OK;

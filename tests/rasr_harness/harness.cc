@@ -137,9 +137,12 @@ u32 idOf(const std::string& type) {
     return id;
 }
 
-Core::Ref<Mm::FeatureScorerScaling> create(const Model& m, const std::string& type, u32 bufferSize) {
+Core::Ref<Mm::FeatureScorerScaling> create(const Model& m, const std::string& type, u32 bufferSize,
+                                           const std::string& shardDevices = "") {
     Core::Configuration root;
     root.set("acoustic-model.mixture-set.buffer-size", std::to_string(bufferSize));
+    if (!shardDevices.empty())
+        root.set("acoustic-model.mixture-set.density-shard-devices", shardDevices);
     const Core::Configuration c(Core::Configuration(root, "acoustic-model"), "mixture-set");
     Mm::FeatureScorer* fs = Mm::Module::instance().featureScorerFactory()->createFeatureScorer(
             idOf(type), c, Core::Ref<const Mm::AbstractMixtureSet>(m.ms.get()));
@@ -154,8 +157,8 @@ const Mm::AssigningFeatureScorer::AssigningContextScorer* unscaled(const Mm::Fea
 }
 
 void runRecognizer(const Model& m, const std::string& type, u32 B, const std::vector<float>& frames, uint32_t F,
-                   uint32_t segments, const Expected& ex) {
-    auto           scorer = create(m, type, B);
+                   uint32_t segments, const Expected& ex, const std::string& shardDevices = "") {
+    auto           scorer = create(m, type, B, shardDevices);
     const uint32_t M = m.ms->nMixtures(), D = m.ms->dimension();
     const bool     assigning = type == "SIMD-diagonal-maximum" || type == "diagonal-maximum";
     uint32_t       t = 0, bad = 0, badBest = 0;
@@ -190,8 +193,9 @@ void runRecognizer(const Model& m, const std::string& type, u32 B, const std::ve
     check(t == F, type + ": every frame fed once");
     check(bad == 0, type + " buffer " + std::to_string(B) + ": " + std::to_string(bad) + " scaled scores differ");
     check(badBest == 0, type + " buffer " + std::to_string(B) + ": " + std::to_string(badBest) + " best densities differ");
-    std::printf("recognizer %-30s buffer-size %5u: %u frames x %u emissions, scores %s, best densities %s\n", type.c_str(), B,
-                F, M, bad ? "DIFFER" : "equal", assigning ? (badBest ? "DIFFER" : "equal") : "n/a");
+    std::printf("recognizer %-30s buffer-size %5u%s: %u frames x %u emissions, scores %s, best densities %s\n", type.c_str(),
+                B, shardDevices.empty() ? "" : (" density-shard-devices " + shardDevices).c_str(), F, M,
+                bad ? "DIFFER" : "equal", assigning ? (badBest ? "DIFFER" : "equal") : "n/a");
 }
 
 void runScoreDump(const Model& m, const std::string& type, u32 B, const std::vector<float>& frames, uint32_t F,
@@ -264,6 +268,8 @@ void checkCriticalErrorRouting(const Model& m, const std::vector<float>& frames)
 
 }  // namespace
 
+extern std::vector<int> gStandinShardDevices;  // gmm_standin.cc
+
 int main() {
     Mm::registerGpuFeatureScorers(0x500);
     Mm::registerGpuFeatureScorers(0x500);  // a second registration of the same ids is refused by the factory
@@ -288,6 +294,14 @@ int main() {
             runRecognizer(model, type, B, frames, F, 3, ex);
             runScoreDump(model, type, B, frames, F, ex);
         }
+    }
+    // "density-shard-devices" reaches gmm_scorer_create_sharded with the configured device list
+    {
+        const Expected ex = oracleScores(model, "SIMD-diagonal-maximum", frames, F);
+        gStandinShardDevices.clear();
+        runRecognizer(model, "SIMD-diagonal-maximum", 64, frames, F, 3, ex, "0,1,2");
+        check(gStandinShardDevices == std::vector<int>({0, 1, 2}), "density-shard-devices -> gmm_scorer_create_sharded");
+        std::printf("density-shard-devices 0,1,2 -> gmm_scorer_create_sharded over %zu devices\n", gStandinShardDevices.size());
     }
     checkCriticalErrorRouting(model, frames);
     std::printf("%s (%d failures)\n", gFailures ? "FAILED" : "PASSED", gFailures);

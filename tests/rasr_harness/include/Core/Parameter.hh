@@ -1,7 +1,9 @@
 // TEST DOUBLE: typed parameters read from a Configuration (Core::ParameterInt / ParameterFloat)
 #pragma once
 #include <cstdlib>
+#include <limits>
 #include <string>
+#include <vector>
 #include "Configuration.hh"
 #include "Assertions.hh"
 #include "Types.hh"
@@ -31,4 +33,34 @@ private:
 };
 typedef Parameter<s32> ParameterInt;
 typedef Parameter<f64> ParameterFloat;
+// Core::ParameterIntVector (Core/Parameter.hh): values split at `delimiter`, each in [min, max]
+class ParameterIntVector {
+public:
+    ParameterIntVector(const char* name, const char* description, const std::string delimiter = " ",
+                       s32 min = std::numeric_limits<s32>::lowest(), s32 max = std::numeric_limits<s32>::max())
+            : name_(name), delimiter_(delimiter.empty() ? " " : delimiter), min_(min), max_(max) { (void)description; }
+    std::vector<s32> operator()(const Configuration& c) const {
+        std::vector<s32> out;
+        std::string      v;
+        if (!c.get(name_, v))
+            return out;
+        size_t b = 0;
+        while (b <= v.size()) {
+            size_t e = v.find(delimiter_, b);
+            if (e == std::string::npos)
+                e = v.size();
+            if (e > b) {
+                const s32 x = static_cast<s32>(std::strtol(v.substr(b, e - b).c_str(), 0, 10));
+                require(x >= min_ && x <= max_);
+                out.push_back(x);
+            }
+            b = e + delimiter_.size();
+        }
+        return out;
+    }
+
+private:
+    std::string name_, delimiter_;
+    s32         min_, max_;
+};
 }  // namespace Core

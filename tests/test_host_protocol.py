@@ -27,7 +27,7 @@ def _write_model(path, ms):
         ms.mixture_log_weights.astype(np.float64).tofile(f)
 
 
-def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, protocol="recognizer"):
+def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, protocol="recognizer", shard_devices=None):
     mp, fp, op = tmp_path / "m.drvmodel", tmp_path / "f.bin", tmp_path / "o.bin"
     if model_file is None:
         _write_model(mp, ms)
@@ -36,8 +36,11 @@ def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, pro
     with open(fp, "wb") as f:
         np.array(frames.shape, dtype=np.uint32).tofile(f)
         frames.astype(np.float32).tofile(f)
+    env = dict(os.environ)
+    if shard_devices:
+        env["RASR_DRIVER_SHARD_DEVICES"] = ",".join(str(d) for d in shard_devices)
     subprocess.run([DRIVER, str(mp), str(fp), str(op), kind, str(buffer_size), str(segments), protocol], check=True,
-                   timeout=300)
+                   timeout=300, env=env)
     raw = np.fromfile(op, dtype=np.uint32)
     F, M, launches = raw[:3]
     s = raw[3:3 + F * M].view(np.float32).reshape(F, M)
@@ -60,6 +63,24 @@ def test_simd_protocol_bit_exact(gpu, tmp_path, buffer_size):
     assert np.array_equal(b.T, ref_b)
     if buffer_size > 1:
         assert launches <= 53  # a launch serves every buffered frame
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("buffer_size", [1, 64])
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "batch-diagonal-maximum-int"])
+def test_density_sharded_protocol_bit_exact(gpu, tmp_path, kind, buffer_size):
+    """The C++ host classes with Configuration::shardDevices (the adapter's "density-shard-devices") = three parts
+    on device 0 (copy exchange): the recognizer protocol bit-exact against the oracle, split mixtures included."""
+    counts = ra.ragged_counts(30, 30 * 9, low=1, high=20, seed=5)
+    ms = ra.synthetic_mixture_set(30, counts, 39, seed=41, weights="random")
+    frames = ra.synthetic_frames(53, 39, seed=42)
+    s, b, _ = _run(tmp_path, ms, frames, kind, buffer_size, 3, shard_devices=[0, 0, 0])
+    if kind == "SIMD-diagonal-maximum":
+        ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+        assert np.array_equal(b.T, ref_b)
+    else:
+        ref_s = oracle.batch_int_score(ms, frames)
+    assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
 
 
 @pytest.mark.gpu

@@ -51,9 +51,11 @@ def test_adapter_linked_and_run_in_plugin_harness():
     plugin machinery (tests/rasr_harness/include/README) over an oracle-backed stand-in of the C-ABI, and driven
     through FeatureScorerFactory, FeatureScorerScaling, the OfflineRecognizer and FeatureScorerNode call
     sequences at buffer sizes 1, 4 and 64 (make check-integration-link): every scaled score and best density
-    equals the oracle's, and a type without assignments routes bestDensity() to the component's criticalError."""
+    equals the oracle's, "density-shard-devices" reaches gmm_scorer_create_sharded, and a type without assignments
+    routes bestDensity() to the component's criticalError."""
     r = subprocess.run(["make", "-s", "-C", ROOT, "check-integration-link"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "PASSED (0 failures)" in r.stdout
-    assert r.stdout.count("score dump") == 10 and r.stdout.count("recognizer") == 10 and "DIFFER" not in r.stdout
+    assert r.stdout.count("score dump") == 10 and r.stdout.count("recognizer ") == 11 and "DIFFER" not in r.stdout
+    assert "density-shard-devices 0,1,2 -> gmm_scorer_create_sharded over 3 devices" in r.stdout
     assert "component criticalError, abort" in r.stdout
