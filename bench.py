@@ -103,6 +103,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (default: the CPUs available)")
     p.add_argument("--cpu-frames-per-thread", type=int, default=3000)
     p.add_argument("--host-boundary", choices=["auto", "off"], default="auto")
+    p.add_argument("--capi-sharded-child", default="",
+                   help="internal: run the C-ABI density-sharded check over these comma-separated devices in this "
+                        "process (started by rank 0 of an N > 1 run) and print one JSON record")
     p.add_argument("--extras", choices=["auto", "off"], default="auto",
                    help="N = 1: device lines at 256/1024/4096 frames per call and the C++ drop-in protocol record")
     return p.parse_args()
@@ -635,8 +638,90 @@ def density_sharded_check(args, ms, ws, rank, local, frames_per_call=4096, calls
         return {"scorer": kind, "error": f"{type(e).__name__}: {e}"[:300]}
 
 
+CAPI_SHARDED_FRAMES = 4096
+
+
+def capi_sharded_child(args):
+    """One process driving several GPUs, as an RASR process with `density-shard-devices` does:
+    gmm_scorer_create_sharded over `--capi-sharded-child` devices (RCCL all-reduce(MIN) exchange when they are
+    distinct: ncclCommInitAll + ncclGroupStart/End, one stream per GPU), on the ragged 800k model (K_m ~ U[64,
+    256]) whose density boundaries split mixtures, so the reduce really runs.  Checked bit for bit (scores and
+    best densities) against the unsharded scorer on device 0; device and host (PCIe-inclusive) calls timed."""
+    import numpy as np
+    import torch
+    import rasr_amd as ra
+    devices = [int(d) for d in args.capi_sharded_child.split(",")]
+    kind, F, calls = "SIMD-diagonal-maximum", CAPI_SHARDED_FRAMES, 8
+    ms = ra.synthetic_mixture_set(args.mixtures, ra.ragged_counts(args.mixtures, args.mixtures * args.densities,
+                                                                  seed=99), args.dim, seed=2025)
+    frames = ra.synthetic_frames(F, args.dim, seed=4242)
+    sh = ra.Scorer(ms, kind, max_frames=F, devices=devices)
+    parts, exchange = sh.shard_info()
+    dev = torch.device("cuda", devices[0])
+    fr = torch.from_numpy(frames).to(dev)
+    s = torch.empty((ms.n_mixtures, F), dtype=torch.float32, device=dev)
+    b = torch.empty((ms.n_mixtures, F), dtype=torch.int32, device=dev)
+    sh.score_device(fr, s, b)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        sh.score_device(fr, s, b)
+    for d in set(devices):
+        torch.cuda.synchronize(torch.device("cuda", d))
+    dev_rate = calls * F / (time.perf_counter() - t0)
+    hs, hb = sh.score_host(frames)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        sh.score_host(frames, out=hs, best_out=hb)
+    host_rate = calls * F / (time.perf_counter() - t0)
+    ref = ra.Scorer(ms, kind, max_frames=F, device=devices[0])
+    rs, rb = ref.score_host(frames)
+    from rasr_amd import parallel
+    split = len(parallel.split_mixtures(parallel.density_shards(ms.mixture_offsets, len(devices))))
+    same = (np.array_equal(s.cpu().numpy().view(np.uint32), rs.view(np.uint32)) and
+            np.array_equal(b.cpu().numpy().view(np.uint32), rb) and np.array_equal(hs.view(np.uint32), rs.view(np.uint32))
+            and np.array_equal(hb, rb))
+    return {"scorer": kind, "api": "gmm_scorer_create_sharded (one process, all GPUs)", "devices": devices,
+            "parts": parts, "exchange": exchange, "split_mixtures": split, "model": "ragged 800k (K_m ~ U[64, 256])",
+            "frames_per_call": F, "device_frames_per_s": dev_rate, "host_frames_per_s": host_rate,
+            "check": "bit-exact vs the unsharded scorer" if same else "MISMATCH vs the unsharded scorer"}
+
+
+def capi_sharded_check(args, ws, rank, timeout_s=300):
+    """N > 1 runs: rank 0 starts `bench.py --capi-sharded-child 0,...,N-1` as a child process (its own HIP
+    contexts and RCCL communicators; bounded by a timeout) while the other ranks wait on a gloo barrier (no
+    GPU work of theirs beside it).  Reported, never fatal to the headline."""
+    import torch
+    import torch.distributed as dist
+    rec = None
+    group = dist.new_group(backend="gloo")
+    if rank == 0:
+        n_vis = torch.cuda.device_count()
+        if n_vis < ws:
+            rec = {"skipped": f"{n_vis} visible devices < {ws} ranks"}
+        else:
+            env = {k: v for k, v in os.environ.items()
+                   if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                                "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+            cmd = [sys.executable, os.path.abspath(__file__), "--capi-sharded-child",
+                   ",".join(str(d) for d in range(ws)), "--mixtures", str(args.mixtures), "--densities",
+                   str(args.densities), "--dim", str(args.dim)]
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+                last = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
+                rec = json.loads(last) if r.returncode == 0 and last.startswith("{") else {
+                    "error": f"child rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+            except subprocess.TimeoutExpired:
+                rec = {"error": f"child timed out after {timeout_s} s"}
+    dist.barrier(group=group)
+    return rec
+
+
 def main():
     args = parse()
+    if args.capi_sharded_child:
+        print(json.dumps(capi_sharded_child(args)), flush=True)
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     if os.environ.get("RASR_BENCH_LAUNCH_PROBE"):  # tests/test_bench_launcher.py: the ranks, no GPU work
@@ -687,6 +772,9 @@ def main():
     dcheck = None
     if ws > 1 and args.parallel == "frames" and args.mode in ("fp32", "simd") and not args.no_density_check:
         dcheck = density_sharded_check(args, ms, ws, rank, local)
+    capi = None
+    if ws > 1 and args.parallel == "frames" and args.mode in ("fp32", "simd") and not args.no_density_check:
+        capi = capi_sharded_check(args, ws, rank)
     cpu = None
     hb = None
     hb_all = None
@@ -746,6 +834,8 @@ def main():
             line["modes"] = extra
         if dcheck is not None:
             line["density_sharded"] = dcheck
+        if capi is not None:
+            line["density_sharded_capi"] = capi
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist

@@ -113,7 +113,10 @@ typedef std::shared_ptr<const ContextScorer> Scorer;   // Core::Ref<const Contex
 
 struct Configuration {
     std::string type               = "SIMD-diagonal-maximum";  // feature-scorer-type (src/Mm/Module.cc:78-80)
-    uint32_t    bufferSize         = 4;     // "buffer-size" (BatchFeatureScorer.cc:28-29)
+    // "buffer-size" (the reference's batch scorers default to 4, BatchFeatureScorer.cc:28-29): 512, the knee of the
+    // measured drop-in throughput (bench.py drop_in_protocol: 64 -> 512 frames +12 %, 512 -> 32768 +1 %; below 64
+    // each launch's ~170 us round trip dominates).  Online decoding that needs scores within a few frames sets 1..4.
+    uint32_t    bufferSize         = 512;
     float       mixtureWeightScale = 1.0f;  // "mixture-weight-scale" (GDMFS.cc:38-40)
     float       gaussianScale      = 1.0f;  // "gaussian-scale" (GDMFS.cc:42-44)
     float       scale              = 1.0f;  // FeatureScorerScaling scale (ScaledFeatureScorer.hh:62-64)

@@ -181,3 +181,20 @@ def test_sharded_refusals(gpu):
         ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=16, devices=[0, 0], mixture_range=(0, 10))
     with pytest.raises(_capi.GmmError):
         ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=16, devices=[0, 0], score_scale=-1.0)
+
+
+@pytest.mark.gpu
+def test_bench_capi_sharded_child(gpu):
+    """bench.py's N > 1 record `density_sharded_capi` (rank 0's child process over all GPUs) on one GPU: three
+    parts on device 0 (copy exchange) of a ragged model, bit-exact against the unsharded scorer."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--capi-sharded-child", "0,0,0",
+                        "--mixtures", "500", "--densities", "40"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["parts"] == 3 and rec["exchange"] == "copy" and rec["split_mixtures"] > 0
+    assert rec["check"] == "bit-exact vs the unsharded scorer", rec
