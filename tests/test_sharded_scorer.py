@@ -75,13 +75,21 @@ def _ragged_model(n_mix=60, total=60 * 14, seed=5):
 
 
 def _compare(kind, ms, frames, s, b, ref_s, ref_b):
+    """Quantized: bit for bit against the unsharded scorer.  Float: the oracle with the float contract
+    (1e-4 relative; diagonal-maximum's best densities may differ only at near ties), as
+    tests/test_density_sharded.py checks the Python layout."""
     if kind in QUANTIZED:
         assert np.array_equal(s.view(np.uint32), ref_s.view(np.uint32))
         if kind == "SIMD-diagonal-maximum":
             assert np.array_equal(b, ref_b)
-    else:
+    elif kind == "diagonal-maximum":
         from test_density_sharded import _check_against_oracle
-        _check_against_oracle(ms, kind, frames, s, b if kind == "diagonal-maximum" else None)
+        _check_against_oracle(ms, kind, frames, s, b)
+    else:
+        import oracle
+        ref = oracle.batch_float_score(ms, frames, n_threads=16)
+        err = np.abs(s.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref.astype(np.float64)))
+        assert err.max() <= 1e-4, f"max rel err {err.max()}"
 
 
 @pytest.mark.gpu
@@ -110,7 +118,8 @@ def test_sharded_one_device_is_unsharded(gpu):
         ref_s, ref_b = ra.Scorer(ms, kind, max_frames=128).score_host(frames)
         s, b = one.score_host(frames)
         assert np.array_equal(s.view(np.uint32), ref_s.view(np.uint32))
-        assert np.array_equal(b, ref_b)
+        if kind in ("SIMD-diagonal-maximum", "diagonal-maximum"):  # batch types write no best densities
+            assert np.array_equal(b, ref_b)
 
 
 @pytest.mark.gpu
