@@ -413,28 +413,39 @@ def available_cpus():
     return n, note
 
 
-def cpu_baseline(args, ms):
+def cpu_baseline(args, ms, repeats=3):
+    """The CPU restatements on the box's permitted cores, each mode's sample split into `repeats` equal runs
+    (the host is shared: one run alone has varied by +-45 % between sessions); value = the median run's rate,
+    the spread reported beside it."""
     import oracle
     import rasr_amd as ra
     threads, note = (args.cpu_threads, "--cpu-threads") if args.cpu_threads else available_cpus()
     out = {}
     for name, per_thread in (("SIMD-diagonal-maximum", args.cpu_frames_per_thread),
                              ("diagonal-maximum", max(1, args.cpu_frames_per_thread // 2))):
-        n = threads * per_thread
+        n = threads * max(1, per_thread // repeats)
         frames = ra.synthetic_frames(n, args.dim, seed=999)
         o = oracle.OracleSimd(ms) if name.startswith("SIMD") else oracle.OracleFloat(ms)
-        t0 = time.perf_counter()
-        o.score(frames, n_threads=threads)
-        dt = time.perf_counter() - t0
-        out[name] = {"value": n / dt, "frames": n, "seconds": dt}
+        rates, total = [], 0.0
+        for _ in range(repeats):
+            t0 = time.perf_counter()
+            o.score(frames, n_threads=threads)
+            dt = time.perf_counter() - t0
+            rates.append(n / dt)
+            total += dt
+        rates.sort()
+        out[name] = {"value": rates[len(rates) // 2], "frames": n * repeats, "seconds": total,
+                     "runs": [round(r, 1) for r in rates]}
         del o
     simd, flt = out["SIMD-diagonal-maximum"], out["diagonal-maximum"]
     return {"value": flt["value"], "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": (f"{flt['frames']} frames x {ms.n_entries} densities, diagonal-maximum restatement "
-                       f"(oracle/gmm_oracle.c orc_float_score, SSE3 distance in the reference's order), {threads} "
-                       f"threads, {flt['seconds']:.1f} s; SIMD-diagonal-maximum restatement (SSE2 u8 SSD like the "
-                       f"reference JIT): {simd['frames']} frames, {simd['seconds']:.1f} s"),
+            "sample": (f"{flt['frames']} frames x {ms.n_entries} densities in {repeats} runs (median), "
+                       f"diagonal-maximum restatement (oracle/gmm_oracle.c orc_float_score, SSE3 distance in the "
+                       f"reference's order), {threads} threads, {flt['seconds']:.1f} s; SIMD-diagonal-maximum "
+                       f"restatement (SSE2 u8 SSD like the reference JIT): {simd['frames']} frames, "
+                       f"{simd['seconds']:.1f} s"),
             "cpu_model": _cpu_model(), "host_logical_cpus": os.cpu_count(), "threads_note": note,
+            "runs": {"diagonal-maximum": flt["runs"], "SIMD-diagonal-maximum": simd["runs"]},
             "modes": {"diagonal-maximum": flt["value"], "SIMD-diagonal-maximum": simd["value"]}}
 
 
