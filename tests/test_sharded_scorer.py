@@ -207,3 +207,32 @@ def test_bench_capi_sharded_child(gpu):
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["parts"] == 3 and rec["exchange"] == "copy" and rec["split_mixtures"] > 0
     assert rec["check"] == "bit-exact vs the unsharded scorer", rec
+
+
+def test_sharded_create_refusals_before_any_device(built):
+    """Argument checks of gmm_scorer_create_sharded that precede any HIP call (run on the CPU): unknown
+    exchange, types whose split mixtures a minimum cannot combine, a mixture range, a non-positive score scale,
+    no devices."""
+    lib = _capi.load_library()
+    ms = _ragged_model()
+    desc = ms.desc()
+    devs = (ctypes.c_int * 2)(0, 0)
+    h = ctypes.c_void_p()
+
+    def create(kind="SIMD-diagonal-maximum", exchange=0, n=2, **cfg_fields):
+        cfg = _capi.ScorerConfig()
+        lib.gmm_default_config(ctypes.byref(cfg))
+        for k, v in cfg_fields.items():
+            setattr(cfg, k, v)
+        return lib.gmm_scorer_create_sharded(ctypes.byref(desc), _capi.SCORER_TYPES[kind], ctypes.byref(cfg), devs, n,
+                                             exchange, ctypes.byref(h))
+
+    assert create(exchange=7) == -1                                  # GMM_ERR_INVALID_ARGUMENT
+    assert create(n=0) == -1
+    for kind in ("diagonal-sum", "preselection-batch-int", "preselection-batch-float"):
+        assert create(kind) == -2, kind                              # GMM_ERR_UNSUPPORTED
+        assert b"minimum" in lib.gmm_last_error()
+    assert create(mixture_begin=0, mixture_end=10) == -2
+    assert create(score_scale=-1.0) == -2
+    assert create(score_scale=0.0) == -2
+    assert not h.value
