@@ -99,6 +99,11 @@ typedef struct {
  * and best densities bit-identical to the reference's arithmetic, at a fraction of the matrix-core
  * kernels' rate.  Dimension <= 128; other types refuse the flag. */
 #define GMM_FLAG_REFERENCE_ORDER 8u
+/* batch-diagonal-maximum-int / -fast (one covariance, dimension <= 64) run a score-only layout by default:
+ * a mixture's rows grouped by the parity of their constant, the constant in the matrix core's accumulator
+ * input, one v_min3 per two candidates (no density index to pack).  Same scores, bit for bit.  This flag
+ * keeps the (score, density) key layout of SIMD-diagonal-maximum instead (A/B timing, tests). */
+#define GMM_FLAG_FULL_KEYS 16u
 
 typedef struct gmm_scorer gmm_scorer;
 

@@ -18,6 +18,7 @@ GMM_FLAG_NATIVE_F32 = 1  # gmm_scorer_config.flags
 GMM_FLAG_SPLIT_TILE16 = 2
 GMM_FLAG_SPLIT_TILE32 = 4
 GMM_FLAG_REFERENCE_ORDER = 8  # diagonal-maximum / batch-float in the reference's f32 operation order
+GMM_FLAG_FULL_KEYS = 16  # batch-int / -fast: (score, density) keys instead of the score-only class layout
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0

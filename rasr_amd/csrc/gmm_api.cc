@@ -115,6 +115,8 @@ struct gmm_scorer {
     uint32_t                lastFrames    = 0;
     // quantized scalars
     uint32_t idxBits = 1, paddedDimension = 0;
+    bool     scoreOnly   = false;    // class layout (batch types): no best densities, cheaper epilogue
+    uint32_t* dMixOddMask = nullptr;
     float    scaling = 0, scalingSquared = 0, invQ = 0, batchScale = 0;
     std::vector<float>    isvScaled;     // [C][D] (quantized types)
     std::vector<uint32_t> mixTileOff;    // host copy
@@ -173,7 +175,7 @@ struct gmm_scorer {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
                         dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
                         dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu, dCentre,
-                        dDirMean, dDirConst, dDirLogNorm, dDirCov, dHostScoresT, dHostBestT};
+                        dDirMean, dDirConst, dDirLogNorm, dDirCov, dHostScoresT, dHostBestT, dMixOddMask};
         for (void* p : ptrs)
             if (p)
                 (void)hipFree(p);
@@ -340,6 +342,8 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.selT        = s->dSelT;
         a.tileClu     = s->dTileClu;
         a.nClusters   = s->clustering.nClusters;
+        a.mixOddMask  = s->dMixOddMask;
+        a.scoreOnly   = s->scoreOnly ? 1 : 0;
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         GMM_HIP_CHECK(launchScoreI8(a, s->kSteps, s->multiCov, stream));
@@ -1014,9 +1018,14 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     int           rc     = GMM_OK;
     if (quantized) {
         PreparedQuantized p;
-        std::string       err = prepareQuantized(*ms, flavor, shard, p);
+        // batch types have no best densities: the score-only class layout where it applies
+        const bool        scoreOnlyLayout = !presel && flavor == Flavor::BatchInt && !(cfg.flags & GMM_FLAG_FULL_KEYS);
+        std::string       err = prepareQuantized(*ms, flavor, shard, p, scoreOnlyLayout);
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
+        s->scoreOnly = p.scoreOnly;
+        if (p.scoreOnly && (rc = upload(&s->dMixOddMask, p.mixOddMask)) != GMM_OK)
+            return rc;
         s->nMix            = p.nMixtures;
         s->kSteps          = p.kSteps;
         s->idxBits         = p.idxBits;

@@ -42,6 +42,10 @@ struct I8Args {
     const void*     tileClu;      // u16 [T+pad][16]: cluster * 64 (byte offset into a wave's mask table)
     uint32_t        nClusters;
     int             presel;
+    // score-only class layout (batch types, gmm_prepare.hh PreparedQuantized::scoreOnly): tileP is the
+    // MFMA's C input, mixOddMask[m] bit g = lane group g holds odd-Q rows
+    const uint32_t* mixOddMask;
+    int             scoreOnly;
 };
 
 struct F32Args {

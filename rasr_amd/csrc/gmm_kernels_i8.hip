@@ -343,11 +343,19 @@ extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 #ifndef GMM_I8_WAVES
 #define GMM_I8_WAVES 4  // scoreI8Seg, one K step: waves per SIMD the register allocation must allow (0 = free)
 #endif
-template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles>
+//
+// SCORE_ONLY (batch types on the class layout, gmm_prepare.cc buildClassLayout): the row constant h = Q >> 1 is
+// the MFMA's C input, so the accumulator holds v = dot + h and the running minimum is one v_min3 per two
+// candidates straight on the accumulators (no pack: there is no density index to carry).  All rows of a lane
+// group have the same parity p of Q within a mixture (bit g of mixOddMask[m]), so the lane's minimum of
+// 2 dot + Q is 2 min(v) + p, formed once per mixture before the cross-lane reduce.
+template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles, bool SCORE_ONLY = false>
 __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_WAVES : 1) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
-                                                   float* __restrict__ scores, uint32_t* __restrict__ bestOut) {
+                                                   float* __restrict__ scores, uint32_t* __restrict__ bestOut,
+                                                   const uint32_t* __restrict__ mixOddMask = nullptr) {
     static_assert(NF == 4 || NF == 8, "NF");
     static_assert(!PRESEL || NF == 4, "preselection masks are 64-frame words");
+    static_assert(!SCORE_ONLY || (!PRESEL && KS == 1), "score-only layout: one K step, no preselection");
     constexpr int      kSegTiles = SEG;
     constexpr int      NPL       = NF / 4;
     constexpr uint32_t kTileA    = KS * 1024;                   // operand bytes per tile
@@ -492,7 +500,9 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     };
     // running minima per column block: every key carries its density index, so the 4 row slots of a
     // lane can share kSlots registers (fewer to reduce and reset at each mixture end)
-    constexpr int kSlots = KS == 1 ? GMM_I8_SLOTS : 4;  // two K steps: 4 (fewer live values to schedule around)
+    // two K steps: 4 (fewer live values to schedule around); SCORE_ONLY: 2 (a chain of dependent v_min3 on one
+    // register costs a wait state per link)
+    constexpr int kSlots = SCORE_ONLY ? 2 : (KS == 1 ? GMM_I8_SLOTS : 4);
     static_assert(kSlots == 1 || kSlots == 2 || kSlots == 4, "slots");
     int best[NF][kSlots];
     const auto resetBest = [&]() {
@@ -505,7 +515,19 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     // hot: the end of a mixture with tiles (its minimum is a real row: no INT_MAX case, unless PRESEL)
     const auto emit = [&](uint32_t mm, auto hot) {
         constexpr bool kMaybeNone = PRESEL || !decltype(hot)::value;
-        if constexpr (PRESEL) {
+        if constexpr (SCORE_ONLY) {
+            if constexpr (decltype(hot)::value) {
+                // this lane group's parity in mixture mm: the minimum of 2 dot + Q is 2 v + p
+                const int p = (static_cast<int>(mixOddMask[mm]) >> g) & 1;
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                    for (int r = 0; r < kSlots; ++r)
+                        best[cb][r] = static_cast<int>((static_cast<uint32_t>(best[cb][r]) << 1) + static_cast<uint32_t>(p));
+            }
+            emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, 0, ssOut);
+        }
+        else if constexpr (PRESEL) {
             int unb[NF][kSlots];
 #pragma unroll
             for (int cb = 0; cb < NF; ++cb)
@@ -566,6 +588,11 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             tileRows(p1, c1, P1, T1w);
             i32x4      accA[NF], accB[NF];
             const auto mfmas = [&](int cb) {
+                if constexpr (SCORE_ONLY) {  // the row constants enter as the accumulator input
+                    accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[0], B[cb][0], P0, 0, 0, 0);
+                    accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[0], B[cb][0], P1, 0, 0, 0);
+                    return;
+                }
                 accA[cb] = i32x4{0, 0, 0, 0};
                 accB[cb] = i32x4{0, 0, 0, 0};
 #pragma unroll
@@ -577,6 +604,11 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             const auto epilogue = [&](int cb) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
+                    if constexpr (SCORE_ONLY) {
+                        int& bs = best[cb][r % kSlots];
+                        asm("v_min3_i32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(accA[cb][r]), "v"(accB[cb][r]));
+                        continue;
+                    }
                     const int ca = cand(accA[cb][r], P0[r], T0w[r], cb), cc = cand(accB[cb][r], P1[r], T1w[r], cb);
                     if constexpr (kSlots < 4) {
                         // several keys into one register: keep each update one v_min3 (the compiler would
@@ -595,18 +627,24 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             // software pipeline over the column blocks: chunks {MFMAs of block cb, epilogue of block cb - 1}
             // fenced by sched_barrier, so every epilogue reads results whose MFMA latency has passed (no
             // hazard s_nop in the stream: 3 wait states per pair step instead of 99; -2.6 % at 32768 frames)
-            mfmas(0);
+            // SCORE_ONLY: the epilogue is 4 v_min3 per block, too short to cover the MFMA latency at lag 1
+            constexpr int kLag = SCORE_ONLY ? 2 : 1;
 #pragma unroll
-            for (int cb = 1; cb < NF; ++cb) {
+            for (int cb = 0; cb < kLag; ++cb)
+                mfmas(cb);
+#pragma unroll
+            for (int cb = kLag; cb < NF; ++cb) {
                 __builtin_amdgcn_sched_barrier(0);
                 mfmas(cb);
-                epilogue(cb - 1);
+                epilogue(cb - kLag);
                 // inside the chunk: the MFMAs first, then the epilogue (the scheduler would lead with the VALU)
                 __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
-            epilogue(NF - 1);
+#pragma unroll
+            for (int cb = NF - kLag; cb < NF; ++cb)
+                epilogue(cb);
             t += two ? 2u : 1u;
             // the mixture ending here, and further ones without tiles ending at the same point (rare)
             if (t == tEnd && m < m1) {
@@ -657,12 +695,19 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
                 attr = true;
             }
             hipLaunchKernelGGL((dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>), dim3(grid), dim3(256), lds, s, a,
-                               a.mixTileOff, a.scores, a.best);
+                               a.mixTileOff, a.scores, a.best, nullptr);
             return;
+        }
+        if constexpr (KS == 1) {
+            if (a.scoreOnly) {  // batch types on the class layout
+                hipLaunchKernelGGL((dev::scoreI8Seg<NF, 1, false, dev::kSegTiles, true>), dim3(grid), dim3(256), 0, s, a,
+                                   a.mixTileOff, a.scores, nullptr, a.mixOddMask);
+                return;
+            }
         }
         // 16-tile segments for one K step (34 KiB per workgroup, 4 per CU); 8 for two (also 34 KiB)
         hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS, false, (KS == 1 ? dev::kSegTiles : 8)>), dim3(grid), dim3(256),
-                           0, s, a, a.mixTileOff, a.scores, a.best);
+                           0, s, a, a.mixTileOff, a.scores, a.best, nullptr);
         return;
     }
 #endif
@@ -674,6 +719,8 @@ hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStr
     if (grid == 0)
         return hipSuccess;
     if (a.presel && (multiCov || !GMM_I8_LDS || a.nClusters == 0 || a.nClusters > 256 || !a.selT || !a.tileClu))
+        return hipErrorInvalidValue;
+    if (a.scoreOnly && (multiCov || kSteps != 1 || !GMM_I8_LDS || a.presel || !a.mixOddMask))
         return hipErrorInvalidValue;
     if (kSteps == 1)
         multiCov ? launchI8T<kI8NF, 1, true>(a, grid, stream) : launchI8T<kI8NF, 1, false>(a, grid, stream);

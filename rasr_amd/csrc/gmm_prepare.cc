@@ -173,7 +173,108 @@ static ShardRange normalizeShard(const gmm_mixture_set& ms, ShardRange s) {
 // quantized scorers: SIMD-diagonal-maximum, batch-diagonal-maximum-int
 // ---------------------------------------------------------------------------
 
-std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out) {
+// Score-only class layout (PreparedQuantized::scoreOnly).  Per mixture, the entries with even and odd
+// Q = c + sum a'^2 go to disjoint lane groups of its tiles (ke groups even, 4 - ke odd, ke chosen for the
+// fewest tiles); a row carries h = Q >> 1 (the MFMA's C input) and -a' as before.  Padding rows carry
+// kClassPadC (never below a real row's v = dot + h, and 2 v + 1 stays inside int32).
+static constexpr int32_t kClassPadC  = 0x30000000;
+static constexpr int64_t kClassLimit = int64_t(1) << 29;  // |2 dot + Q| bound of a real row
+
+// false: some row's |2 dot + Q| may reach kClassLimit; the key layout is used instead
+static bool classLayoutFits(const gmm_mixture_set& ms, ShardRange shard, const PreparedQuantized& out) {
+    const uint32_t D = out.dimension, Dp = out.paddedDimension;
+    for (uint32_t x = ms.mixture_offsets[shard.begin]; x < ms.mixture_offsets[shard.end]; ++x) {
+        const uint8_t* pm    = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
+        int64_t        sumSq = 0, sumAbs = 0;
+        for (uint32_t k = 0; k < D; ++k) {
+            const int64_t an = 128 - static_cast<int32_t>(pm[k]);
+            if (an > 127)
+                return false;  // mean quantized to 0: not an s8 operand (the key layout reports it)
+            sumSq += an * an;
+            sumAbs += an < 0 ? -an : an;
+        }
+        const int64_t q = static_cast<int64_t>(out.constantWeight[x]) + sumSq;
+        if ((q < 0 ? -q : q) + 2 * 128 * sumAbs >= kClassLimit)
+            return false;
+    }
+    return true;
+}
+
+static std::string buildClassLayout(const gmm_mixture_set& ms, ShardRange shard, PreparedQuantized& out) {
+    const uint32_t D = out.dimension, Dp = out.paddedDimension, nMix = shard.end - shard.begin;
+    Tiling&        t = out.tiling;
+    t                = Tiling();
+    t.mixTileOffset.assign(nMix + 1, 0);
+    out.mixOddMask.assign(nMix, 0);
+    out.tileA.clear();
+    out.tileP.clear();
+    std::vector<uint32_t> cls[2];
+    for (uint32_t mi = 0; mi < nMix; ++mi) {
+        const uint32_t m = shard.begin + mi;
+        const uint32_t b = ms.mixture_offsets[m], e = ms.mixture_offsets[m + 1];
+        t.maxEntriesPerMixture = std::max(t.maxEntriesPerMixture, e - b);
+        cls[0].clear();
+        cls[1].clear();
+        for (uint32_t x = b; x < e; ++x) {
+            const uint8_t* pm    = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
+            int64_t        sumSq = 0, sumAbs = 0;
+            for (uint32_t k = 0; k < D; ++k) {
+                const int64_t an = 128 - static_cast<int32_t>(pm[k]);
+                sumSq += an * an;
+                sumAbs += an < 0 ? -an : an;
+            }
+            (void)sumAbs;  // range checked by classLayoutFits
+            const int64_t q = static_cast<int64_t>(out.constantWeight[x]) + sumSq;
+            cls[static_cast<uint64_t>(q) & 1u].push_back(x);
+        }
+        const uint32_t nE = static_cast<uint32_t>(cls[0].size()), nO = static_cast<uint32_t>(cls[1].size());
+        // lane groups for the even class: the fewest tiles (4 rows per lane group per tile)
+        uint32_t ke = nO == 0 ? 4u : (nE == 0 ? 0u : 2u), tiles = UINT32_MAX;
+        for (uint32_t k = (nE ? 1u : 0u); k <= (nO ? 3u : 4u); ++k) {
+            const uint32_t te = k ? (nE + 4 * k - 1) / (4 * k) : 0, to = k < 4 ? (nO + 4 * (4 - k) - 1) / (4 * (4 - k)) : 0;
+            if (std::max(te, to) < tiles)
+                tiles = std::max(te, to), ke = k;
+        }
+        if (nE + nO == 0)
+            tiles = 0;
+        out.mixOddMask[mi] = (0xfu << ke) & 0xfu;
+        const uint32_t t0 = t.nTiles;
+        t.nTiles += tiles;
+        out.tileA.resize(static_cast<size_t>(t.nTiles) * kLanes * 16, 0);
+        out.tileP.resize(static_cast<size_t>(t.nTiles) * kTileRows, kClassPadC);
+        t.rowEntry.resize(static_cast<size_t>(t.nTiles) * kTileRows, UINT32_MAX);
+        t.rowDensityInMixture.resize(static_cast<size_t>(t.nTiles) * kTileRows, UINT32_MAX);
+        t.tileCovariance.resize(t.nTiles, 0);
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t g0 = c ? ke : 0, ng = c ? 4 - ke : ke;  // lane groups of the class
+            for (size_t i = 0; i < cls[c].size(); ++i) {
+                const uint32_t x    = cls[c][i];
+                const uint32_t tile = t0 + static_cast<uint32_t>(i / (4 * ng));
+                const uint32_t slot = static_cast<uint32_t>(i % (4 * ng));
+                const uint32_t r    = 4 * (g0 + slot / 4) + slot % 4;  // rows 4g..4g+3 belong to lane group g
+                const uint8_t* pm   = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
+                int64_t        sumSq = 0;
+                for (uint32_t k = 0; k < D; ++k) {
+                    const int32_t an = 128 - static_cast<int32_t>(pm[k]);
+                    sumSq += static_cast<int64_t>(an) * an;
+                    const uint32_t lane = (k / 16) * 16 + r, j = k % 16;  // one K step: k < 64
+                    out.tileA[(static_cast<size_t>(tile) * kLanes + lane) * 16 + j] = static_cast<int8_t>(an);
+                }
+                const int64_t q = static_cast<int64_t>(out.constantWeight[x]) + sumSq;
+                out.tileP[static_cast<size_t>(tile) * kTileRows + r] = static_cast<int32_t>(q >> 1);  // floor
+                t.rowEntry[static_cast<size_t>(tile) * kTileRows + r]            = x;
+                t.rowDensityInMixture[static_cast<size_t>(tile) * kTileRows + r] = x - ms.mixture_offsets[shard.begin + mi];
+            }
+        }
+        t.mixTileOffset[mi + 1] = t.nTiles;
+    }
+    out.idxBits   = 0;
+    out.scoreOnly = true;
+    return "";
+}
+
+std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out,
+                             bool scoreOnlyLayout) {
     std::string err = validate(ms);
     if (!err.empty())
         return err;
@@ -257,6 +358,13 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
         }
     }
 
+    out.isvDevice.assign(static_cast<size_t>(C) * out.kSteps * kI8K, 0.0f);
+    for (uint32_t c = 0; c < C; ++c)
+        for (uint32_t k = 0; k < D; ++k)
+            out.isvDevice[static_cast<size_t>(c) * out.kSteps * kI8K + k] = out.isvScaled[static_cast<size_t>(c) * D + k];
+    if (scoreOnlyLayout && C == 1 && out.kSteps == 1 && classLayoutFits(ms, shard, out))
+        return buildClassLayout(ms, shard, out);
+
     // device tiles
     buildTiling(ms, shard, out.tiling);
     uint32_t ib = 1;
@@ -304,10 +412,6 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
                     static_cast<int32_t>(biasv * (static_cast<int64_t>(1) << ib) + dnsIdx);
         }
     }
-    out.isvDevice.assign(static_cast<size_t>(C) * KS * kI8K, 0.0f);
-    for (uint32_t c = 0; c < C; ++c)
-        for (uint32_t k = 0; k < D; ++k)
-            out.isvDevice[static_cast<size_t>(c) * KS * kI8K + k] = out.isvScaled[static_cast<size_t>(c) * D + k];
     return "";
 }
 

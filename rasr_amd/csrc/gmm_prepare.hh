@@ -77,6 +77,12 @@ struct PreparedQuantized {
     std::vector<int8_t>  tileA;       // [nTiles][kSteps][64 lanes][16]
     std::vector<int32_t> tileP;       // [nTiles][16]
     std::vector<float>   isvDevice;   // [C][kSteps*64], zero padded
+    // score-only class layout (batch types: no best density; one covariance, one K step): a mixture's rows
+    // are split by the parity of Q = c + sum a'^2 over the tile's 4 lane groups (bit g of mixOddMask[m]:
+    // lane group g holds odd-Q rows), and tileP holds the MFMA's C input h = Q >> 1, so the accumulator is
+    // v = dot + h and the row value 2 dot + Q = 2 v + p with p fixed per lane group (gmm_kernels_i8.hip)
+    bool                 scoreOnly = false;
+    std::vector<uint32_t> mixOddMask;  // [nMixtures]
 };
 
 struct PreparedFloat {
@@ -131,7 +137,9 @@ struct PreparedDirect {
 
 // Returns empty string on success, else an error message.
 std::string validate(const gmm_mixture_set& ms);
-std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out);
+// scoreOnlyLayout: lay out the class layout above when it applies (out.scoreOnly says whether it did)
+std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out,
+                             bool scoreOnlyLayout = false);
 // wantSplit: lay the model out for the split-f16 kernel when it applies (one covariance,
 // 3*dimension+7 <= 256, row constants below 2^30); out.split says whether it did.
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,

@@ -3,8 +3,9 @@
 
 Each variant runs in its own subprocess (RASR_GMM_LIB=<so>); rounds are interleaved
 (v1 v2 ... v1 v2 ...) and the median / min kernel time per variant is reported.
-usage: ab_bench.py --mode fp32|simd|sum --rounds 3 lib1.so lib2.so[:split16|:split32] ...
-(":split16" / ":split32" run that library with GMM_FLAG_SPLIT_TILE16 / _TILE32)
+usage: ab_bench.py --mode fp32|simd|sum|bint --rounds 3 lib1.so lib2.so[:split16|:split32|:fullkeys] ...
+(":split16" / ":split32" run that library with GMM_FLAG_SPLIT_TILE16 / _TILE32, ":fullkeys" with GMM_FLAG_FULL_KEYS;
+bint = batch-diagonal-maximum-int, scores only)
 """
 import argparse
 import json
@@ -20,20 +21,23 @@ import os, sys, json, time
 sys.path.insert(0, os.environ["ROOT"])
 import torch, rasr_amd as ra
 mode = os.environ["MODE"]; F = int(os.environ["FRAMES"])
-kind = {"fp32": "diagonal-maximum", "simd": "SIMD-diagonal-maximum", "sum": "diagonal-sum"}[mode]
+kind = {"fp32": "diagonal-maximum", "simd": "SIMD-diagonal-maximum", "sum": "diagonal-sum",
+        "bint": "batch-diagonal-maximum-int"}[mode]
 D = int(os.environ.get("DIM", "39"))
 ms = ra.synthetic_mixture_set(5000, 160, D, seed=2024)
-sc = ra.Scorer(ms, kind, max_frames=F, split_tile16=os.environ.get("SPLIT") == "16",
-               split_tile32=os.environ.get("SPLIT") == "32")
+opt = os.environ.get("OPT", "")
+sc = ra.Scorer(ms, kind, max_frames=F, split_tile16=opt == "split16", split_tile32=opt == "split32",
+               full_keys=opt == "fullkeys")
 fr = torch.from_numpy(ra.synthetic_frames(F, D, seed=5)).cuda()
 out = torch.empty((5000, F), dtype=torch.float32, device="cuda")
-best = torch.empty((5000, F), dtype=torch.int32, device="cuda")
+best = (torch.zeros((5000, F), dtype=torch.int32, device="cuda") if mode != "bint" else None)
 for _ in range(3): sc.score_device(fr, out, best)
 torch.cuda.synchronize(); sc.set_timing(True)
 for _ in range(int(os.environ["STEPS"])): sc.score_device(fr, out, best)
 ms_, n = sc.kernel_time()
 w = torch.arange(1, F + 1, device="cuda", dtype=torch.int64) * 2654435761 % 1000003
-h = int(((out.view(torch.int32).long() + 7 * best.long()) * w).sum(dim=1).remainder(2**61 - 1).sum())
+key = out.view(torch.int32).long() + (7 * best.long() if best is not None else 0)
+h = int((key * w).sum(dim=1).remainder(2**61 - 1).sum())
 print(json.dumps({"kernel_ms": ms_ / n, "checksum": float(out[:, :64].double().sum()), "hash": h}))
 '''
 
@@ -54,7 +58,7 @@ def main():
         for lib in a.libs:
             path, _, opt = lib.partition(":")
             env = dict(os.environ, RASR_GMM_LIB=os.path.abspath(path), ROOT=ROOT, MODE=a.mode, FRAMES=str(frames),
-                       STEPS=str(a.steps), DIM=str(a.dim), SPLIT=opt.replace("split", ""))
+                       STEPS=str(a.steps), DIM=str(a.dim), OPT=opt)
             p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 print(lib, "FAILED", p.stderr[-2000:])
