@@ -64,6 +64,8 @@ VOP3_CYCLES = 3.14                    # measured issue cost of a 3-source VOP3 p
 MODES = {
     "fp32": ("diagonal-maximum", "f32"),
     "simd": ("SIMD-diagonal-maximum", "s8xs8->i32 (u8-quantized, bit-exact)"),
+    # batched int scorer (no best densities): the score-only class layout (gmm_prepare.cc buildClassLayout)
+    "bint": ("batch-diagonal-maximum-int", "s8xs8->i32 (u8-quantized, bit-exact)"),
     "sum": ("diagonal-sum", "f32"),  # log-sum-exp variant (GaussDiagonalSumFeatureScorer), --mode sum
     "nn": ("nn-batch-feature-scorer", "bf16 x bf16 -> f32 (MFMA), f32 bias/activation"),  # config 5, --mode nn
     # density preselection (256 clusters, 32 selected per frame): cluster selection + masked scoring
@@ -72,7 +74,7 @@ MODES = {
 }
 FRAMES_PER_LAUNCH = 32768  # frames per scorer call (the scorer's max_frames)
 # scorer calls per step: about 50-60 ms of GPU work per step at the measured rates, so 20 steps >= 1 s
-DEFAULT_LAUNCHES = {"fp32": 12, "simd": 32, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
+DEFAULT_LAUNCHES = {"fp32": 12, "simd": 32, "bint": 40, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
 # BASELINE config 5 network (hybrid DNN): 11 x 39 spliced MFCC input, 6 sigmoid layers of 2048, 5000 classes
 NN_DIMS = [429] + [2048] * 6 + [5000]
 
@@ -222,7 +224,7 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         seed = 1000 + rank
     m_local = sc.n_mixtures()
     frames = torch.from_numpy(ra.synthetic_frames(f_step, args.dim, seed=seed)).to(dev)
-    want_best = not (args.no_best or mode.startswith("presel"))
+    want_best = not (args.no_best or mode.startswith("presel") or mode == "bint")  # batch types: no best
     scores = torch.empty((m_local, f_step if not sharded else fpl), dtype=torch.float32, device=dev)
     best = (torch.empty((m_local, f_step if not sharded else fpl), dtype=torch.int32, device=dev)
             if want_best else None)
@@ -310,12 +312,14 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         # the quantized scorer is reported against max(t_MFMA, t_VALU).  Its epilogue is one
         # 3-source VOP3 (v_lshl_add) per (frame, density) plus half a v_min3; a wave64 VOP3 issues every
         # VOP3_CYCLES cycles per SIMD with 4 waves per SIMD (scripts/debug/vgpr_banks.hip)
-        keys_per_s = N_SIMDS * CLOCK_GHZ * 1e9 * 64.0 / (1.5 * VOP3_CYCLES)
+        # The score-only class layout (batch types) has no pack: half a v_min3 per (frame, density)
+        vop3 = 0.5 if mode == "bint" else 1.5
+        keys_per_s = N_SIMDS * CLOCK_GHZ * 1e9 * 64.0 / (vop3 * VOP3_CYCLES)
         ceiling = keys_per_s / d_local
         res["roofline"]["valu"] = {
             "ceiling_frames_per_s": ceiling,
             "frac": (fpl / sec) / ceiling,
-            "basis": f"1.5 VOP3 per (frame, density), {VOP3_CYCLES} cycles per wave64 VOP3 per SIMD, "
+            "basis": f"{vop3} VOP3 per (frame, density), {VOP3_CYCLES} cycles per wave64 VOP3 per SIMD, "
                      f"{N_SIMDS} SIMDs at {CLOCK_GHZ} GHz",
         }
     del sc, scores, best, frames
@@ -774,12 +778,13 @@ def main():
     res = run_mode(args, args.mode, ms, ws, rank, local, launches)
     extra = {}
     if not args.no_extra_mode:
-        other = "simd" if args.mode != "simd" else "fp32"  # (nn returned above)
-        r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_LAUNCHES[other])
-        extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
-                        "frames_per_gpu_per_step": r2["frames_per_step"], "frames_per_launch": r2["frames_per_launch"],
-                        "timed_region_s": r2["timed_region_s"], "dtype": r2["dtype"],
-                        "scorer": MODES[other][0], "roofline": r2["roofline"]}
+        # the other headline-model scorers (nn returned above): fp32 / SIMD, and the batched int scorer
+        for other in [m for m in ("fp32", "simd", "bint") if m != args.mode]:
+            r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_LAUNCHES[other])
+            extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
+                            "frames_per_gpu_per_step": r2["frames_per_step"],
+                            "frames_per_launch": r2["frames_per_launch"], "timed_region_s": r2["timed_region_s"],
+                            "dtype": r2["dtype"], "scorer": MODES[other][0], "roofline": r2["roofline"]}
     dcheck = None
     if ws > 1 and args.parallel == "frames" and args.mode in ("fp32", "simd") and not args.no_density_check:
         dcheck = density_sharded_check(args, ms, ws, rank, local)
@@ -824,7 +829,7 @@ def main():
                 "dimension": args.dim,
                 "frames_per_gpu_per_step": res["frames_per_step"],
                 "frames_per_launch": res["frames_per_launch"],
-                "best_density": not args.no_best and not args.mode.startswith("presel"),
+                "best_density": not args.no_best and not args.mode.startswith("presel") and args.mode != "bint",
                 "parallelism": (f"mixture-sharded x{ws} + RCCL all-gather" if args.parallel == "mixtures" and ws > 1
                                 else f"density-sharded x{ws} + RCCL all-reduce(MIN) of split mixtures + all-gather"
                                 if args.parallel == "densities" and ws > 1 else f"frame-sharded replicas x{ws}"),
