@@ -605,8 +605,12 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if constexpr (SCORE_ONLY) {
+                        // a compiler-visible min (not inline asm): the accumulators are read soon after their
+                        // MFMAs, and only compiler-visible reads get the hazard wait states.  The empty asm keeps
+                        // each update one v_min3 (the compiler would reassociate the chain into v_min pairs)
                         int& bs = best[cb][r % kSlots];
-                        asm("v_min3_i32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(accA[cb][r]), "v"(accB[cb][r]));
+                        bs      = min(bs, min(accA[cb][r], accB[cb][r]));
+                        asm volatile("" : "+v"(bs));
                         continue;
                     }
                     const int ca = cand(accA[cb][r], P0[r], T0w[r], cb), cc = cand(accB[cb][r], P1[r], T1w[r], cb);
@@ -627,24 +631,28 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             // software pipeline over the column blocks: chunks {MFMAs of block cb, epilogue of block cb - 1}
             // fenced by sched_barrier, so every epilogue reads results whose MFMA latency has passed (no
             // hazard s_nop in the stream: 3 wait states per pair step instead of 99; -2.6 % at 32768 frames)
-            // SCORE_ONLY: the epilogue is 4 v_min3 per block, too short to cover the MFMA latency at lag 1
-            constexpr int kLag = SCORE_ONLY ? 2 : 1;
+            // SCORE_ONLY: the epilogue is 4 v_min3 per block, too short to cover the MFMA latency at lag 1; lag 3
+            // leaves the compiler the fewest hazard waits (A/B, 32768 frames: lag 3 1.338 ms, lag 2 1.341, a
+            // separate single-tile step for odd tile counts 1.362)
+            constexpr int kLag = SCORE_ONLY ? 3 : 1;
+            {
 #pragma unroll
-            for (int cb = 0; cb < kLag; ++cb)
-                mfmas(cb);
+                for (int cb = 0; cb < kLag; ++cb)
+                    mfmas(cb);
 #pragma unroll
-            for (int cb = kLag; cb < NF; ++cb) {
+                for (int cb = kLag; cb < NF; ++cb) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfmas(cb);
+                    epilogue(cb - kLag);
+                    // inside the chunk: the MFMAs first, then the epilogue (the scheduler would lead with the VALU)
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);
-                mfmas(cb);
-                epilogue(cb - kLag);
-                // inside the chunk: the MFMAs first, then the epilogue (the scheduler would lead with the VALU)
-                __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int cb = NF - kLag; cb < NF; ++cb)
-                epilogue(cb);
+                for (int cb = NF - kLag; cb < NF; ++cb)
+                    epilogue(cb);
+            }
             t += two ? 2u : 1u;
             // the mixture ending here, and further ones without tiles ending at the same point (rare)
             if (t == tEnd && m < m1) {
