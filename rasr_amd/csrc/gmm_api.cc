@@ -890,12 +890,18 @@ int groupScore(gmm_scorer* s, const float* frames, uint32_t n, uint32_t frameStr
     const int64_t* reduced = nullptr;
     if (nS && g.exchange == GMM_EXCHANGE_RCCL) {
         GMM_NCCL_CHECK(ncclGroupStart());
-        for (uint32_t i = 0; i < P; ++i) {
+        ncclResult_t nr = ncclSuccess;
+        hipError_t   hr = hipSuccess;
+        for (uint32_t i = 0; i < P && nr == ncclSuccess && hr == hipSuccess; ++i) {
             DensityPart& p = g.parts[i];
-            GMM_HIP_CHECK(hipSetDevice(p.device));
-            GMM_NCCL_CHECK(ncclAllReduce(p.dKeys, p.dKeys, keyN, ncclInt64, ncclMin, g.comms[i], p.stream));
+            if ((hr = hipSetDevice(p.device)) == hipSuccess)
+                nr = ncclAllReduce(p.dKeys, p.dKeys, keyN, ncclInt64, ncclMin, g.comms[i], p.stream);
         }
-        GMM_NCCL_CHECK(ncclGroupEnd());
+        const ncclResult_t ne = ncclGroupEnd();  // always closes the group, also after a failed enqueue
+        if (hr != hipSuccess)
+            return fail(GMM_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(hr));
+        GMM_NCCL_CHECK(nr);
+        GMM_NCCL_CHECK(ne);
         reduced = g.parts[0].dKeys;  // part 0 is on the lead device
     }
     else if (nS) {
