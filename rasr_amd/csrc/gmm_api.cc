@@ -230,12 +230,21 @@ int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
 #ifndef GMM_TARGET_BLOCKS
 #define GMM_TARGET_BLOCKS 8192
 #endif
-    // RASR_GMM_TARGET_BLOCKS: tuning override (scripts/sweep_chunks.sh)
-    static const uint32_t kTargetBlocks = [] {
+    // RASR_GMM_TARGET_BLOCKS: tuning override (scripts/sweep_chunks.sh, scripts/sweep_small_batches.sh)
+    static const uint32_t kOverride = [] {
         const char* e = std::getenv("RASR_GMM_TARGET_BLOCKS");
         const long  v = e ? std::strtol(e, nullptr, 10) : 0;
-        return v > 0 ? static_cast<uint32_t>(v) : uint32_t(GMM_TARGET_BLOCKS);
+        return v > 0 ? static_cast<uint32_t>(v) : 0u;
     }();
+    // Small calls (few frame tiles) with many one-mixture chunks reload the frame operands once per mixture:
+    // fewer, larger chunks there (measured, profiles/r03/sweep_small_batches.txt: split kernel at 256 frames
+    // 0.048 ms with 1024 blocks vs 0.063 with 8192, at 1024 frames 0.160 vs 0.175; quantized kernel at 1024
+    // frames 0.0695 with 2048 vs 0.0729); large calls keep GMM_TARGET_BLOCKS
+    const uint32_t kTargetBlocks =
+            kOverride ? kOverride
+            : s->split ? std::clamp<uint32_t>(nFrameTiles * 256u, 1024u, uint32_t(GMM_TARGET_BLOCKS))
+            : s->quantized && !s->presel ? std::clamp<uint32_t>(nFrameTiles * 1024u, 2048u, uint32_t(GMM_TARGET_BLOCKS))
+                                         : uint32_t(GMM_TARGET_BLOCKS);
     uint32_t       target        = std::max<uint32_t>(1, (kTargetBlocks + nFrameTiles - 1) / nFrameTiles);
     target                       = std::min<uint32_t>(target, std::max<uint32_t>(1, s->nMix));
     const uint32_t T             = s->nTiles;
