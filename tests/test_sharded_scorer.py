@@ -236,3 +236,18 @@ def test_sharded_create_refusals_before_any_device(built):
     assert create(score_scale=-1.0) == -2
     assert create(score_scale=0.0) == -2
     assert not h.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "batch-diagonal-maximum-int"])
+def test_sharded_host_pipeline_chunks(gpu, kind):
+    """A host call large enough for the chunked copy-out pipeline (table >= 8 MB, >= 2 x 8192 frames): every
+    frame chunk runs the whole group (parts, key exchange, assembly) before its copy-out."""
+    counts = ra.ragged_counts(200, 200 * 12, low=1, high=24, seed=21)
+    ms = ra.synthetic_mixture_set(200, counts, 39, seed=22, weights="random")
+    frames = ra.synthetic_frames(16500, 39, seed=23)
+    ref_s, ref_b = ra.Scorer(ms, kind, max_frames=16500).score_host(frames)
+    s, b = ra.Scorer(ms, kind, max_frames=16500, devices=[0, 0, 0]).score_host(frames)
+    assert np.array_equal(s.view(np.uint32), ref_s.view(np.uint32))
+    if kind.startswith("SIMD"):
+        assert np.array_equal(b, ref_b)
