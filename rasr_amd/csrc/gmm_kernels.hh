@@ -4,8 +4,29 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
+#include <set>
+#include <utility>
 
 namespace rasr_gmm {
+
+// hipFuncAttributeMaxDynamicSharedMemorySize for `fn` on the current device, once per (kernel, device): a
+// process may drive several GPUs (gmm_scorer_create_sharded, one handle per GPU), and the attribute belongs to
+// the device's copy of the kernel
+inline hipError_t allowDynamicLds(const void* fn, int bytes) {
+    static std::mutex                        mu;
+    static std::set<std::pair<const void*, int>> done;
+    int                                      dev = 0;
+    hipError_t                               e   = hipGetDevice(&dev);
+    if (e != hipSuccess)
+        return e;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({fn, dev}))
+        return hipSuccess;
+    if ((e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) == hipSuccess)
+        done.insert({fn, dev});
+    return e;
+}
 
 #ifndef GMM_I8_NF
 #define GMM_I8_NF 8

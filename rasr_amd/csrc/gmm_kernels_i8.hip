@@ -695,13 +695,8 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
             constexpr int      kSeg  = 4;
             constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 32)) + kI8DummyTileBytes(KS, true);
             const uint32_t     lds   = kRing + 64u + 4u * a.nClusters * 16u;
-            static bool        attr  = false;
-            if (!attr) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          static_cast<int>(kRing + 4u * 256u * 64u));
-                attr = true;
-            }
+            (void)allowDynamicLds(reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>),
+                                  static_cast<int>(kRing + 4u * 256u * 64u));
             hipLaunchKernelGGL((dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>), dim3(grid), dim3(256), lds, s, a,
                                a.mixTileOff, a.scores, a.best, nullptr);
             return;

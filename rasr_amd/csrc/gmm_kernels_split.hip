@@ -958,12 +958,8 @@ template <int KS>
 static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
     if (a.presel) {  // preselection-batch-float: no best density; the waves' mask tables in dynamic LDS
         const uint32_t lds = kSplitWaves * a.nClusters * 64u;
-        static bool    attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::scoreSplit<KS, false, true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSplitWaves * 256u * 64u));
-            attr = true;
-        }
+        (void)allowDynamicLds(reinterpret_cast<const void*>(&dev::scoreSplit<KS, false, true>),
+                              static_cast<int>(kSplitWaves * 256u * 64u));
         hipLaunchKernelGGL((dev::scoreSplit<KS, false, true>), dim3(grid), dim3(64 * kSplitWaves), lds, s, a,
                            a.mixTileOff);
     }

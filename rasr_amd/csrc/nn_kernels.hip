@@ -10,6 +10,7 @@
 // output-unit tiles of one frame tile (its activations stay in that XCD's L2).  The variants measured
 // against it (a 128 x 128 tile, the two-half schedule, a persistent form, 32x32x16 quadrants, s_setprio
 // modes) are kept out of this file: scripts/variants/.
+#include "gmm_kernels.hh"  // rasr_gmm::allowDynamicLds
 #include "nn_kernels.hh"
 
 #include <algorithm>
@@ -366,14 +367,9 @@ hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream) {
     if (nwg == 0)
         return hipSuccess;
     constexpr uint32_t kLds = 2u * 2u * 256u * 64u * 2u;  // 128 KiB
-    static bool        attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::nnGemm8p),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLds));
-        if (e != hipSuccess)
-            return e;
-        attr = true;
-    }
+    const hipError_t e = rasr_gmm::allowDynamicLds(reinterpret_cast<const void*>(&dev::nnGemm8p), static_cast<int>(kLds));
+    if (e != hipSuccess)
+        return e;
     hipLaunchKernelGGL(dev::nnGemm8p, dim3(nwg), dim3(512), kLds, stream, a);
     return hipGetLastError();
 }
