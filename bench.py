@@ -66,6 +66,10 @@ MODES = {
     "simd": ("SIMD-diagonal-maximum", "s8xs8->i32 (u8-quantized, bit-exact)"),
     # batched int scorer (no best densities): the score-only class layout (gmm_prepare.cc buildClassLayout)
     "bint": ("batch-diagonal-maximum-int", "s8xs8->i32 (u8-quantized, bit-exact)"),
+    # the assigning scorers without best densities (the search reads only score(e)): SIMD on its score-only
+    # twin (class layout), fp32 without the index tag
+    "simd-scores": ("SIMD-diagonal-maximum", "s8xs8->i32 (u8-quantized, bit-exact)"),
+    "fp32-scores": ("diagonal-maximum", "f32"),
     "sum": ("diagonal-sum", "f32"),  # log-sum-exp variant (GaussDiagonalSumFeatureScorer), --mode sum
     "nn": ("nn-batch-feature-scorer", "bf16 x bf16 -> f32 (MFMA), f32 bias/activation"),  # config 5, --mode nn
     # density preselection (256 clusters, 32 selected per frame): cluster selection + masked scoring
@@ -74,7 +78,7 @@ MODES = {
 }
 FRAMES_PER_LAUNCH = 32768  # frames per scorer call (the scorer's max_frames)
 # scorer calls per step: about 50-60 ms of GPU work per step at the measured rates, so 20 steps >= 1 s
-DEFAULT_LAUNCHES = {"fp32": 12, "simd": 32, "bint": 40, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
+DEFAULT_LAUNCHES = {"fp32": 12, "simd": 32, "bint": 40, "simd-scores": 40, "fp32-scores": 12, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
 # BASELINE config 5 network (hybrid DNN): 11 x 39 spliced MFCC input, 6 sigmoid layers of 2048, 5000 classes
 NN_DIMS = [429] + [2048] * 6 + [5000]
 
@@ -224,7 +228,8 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         seed = 1000 + rank
     m_local = sc.n_mixtures()
     frames = torch.from_numpy(ra.synthetic_frames(f_step, args.dim, seed=seed)).to(dev)
-    want_best = not (args.no_best or mode.startswith("presel") or mode == "bint")  # batch types: no best
+    # batch types: no best; the -scores modes: the assigning types asked for scores only
+    want_best = not (args.no_best or mode.startswith("presel") or mode == "bint" or mode.endswith("-scores"))
     scores = torch.empty((m_local, f_step if not sharded else fpl), dtype=torch.float32, device=dev)
     best = (torch.empty((m_local, f_step if not sharded else fpl), dtype=torch.int32, device=dev)
             if want_best else None)
@@ -271,7 +276,7 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         kq = 16 if kernel == "scoreSplit32" else 32
         k_issued = kq * ((3 * args.dim + 7 + kq - 1) // kq)
         issued = 2.0 * k_issued * d_local * fpl
-    elif mode in ("fp32", "sum"):
+    elif mode in ("fp32", "fp32-scores", "sum"):
         peak = PEAK_F32_MFMA_TFLOPS
         issued = 2.0 * 4 * ((args.dim + 1 + 3) // 4) * d_local * fpl
     else:
@@ -313,7 +318,7 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         # 3-source VOP3 (v_lshl_add) per (frame, density) plus half a v_min3; a wave64 VOP3 issues every
         # VOP3_CYCLES cycles per SIMD with 4 waves per SIMD (scripts/debug/vgpr_banks.hip)
         # The score-only class layout (batch types) has no pack: half a v_min3 per (frame, density)
-        vop3 = 0.5 if mode == "bint" else 1.5
+        vop3 = 0.5 if (mode == "bint" or (mode == "simd-scores" and best is None)) else 1.5
         keys_per_s = N_SIMDS * CLOCK_GHZ * 1e9 * 64.0 / (vop3 * VOP3_CYCLES)
         ceiling = keys_per_s / d_local
         res["roofline"]["valu"] = {
@@ -456,8 +461,9 @@ def cpu_baseline(args, ms, repeats=3):
 def host_boundary(args, ms, kind, calls=6):
     """gmm_score_host (host frames in, host tables out, PCIe included) into page-locked tables
     (rasr_amd.pinned_empty = gmm_host_alloc), the path an RASR caller reading score(e) on the host takes:
-    score + best tables, scores only (best densities kept on the device, GMM_HOST_KEEP_BEST: what the search
-    needs), and scores only frame-major (GMM_HOST_FRAME_MAJOR, the drop-in's own table layout)."""
+    score + best tables, scores only (GMM_HOST_LAZY_BEST: best densities computed only if fetched later, what the
+    search needs and what the C++ drop-in asks for), and scores only frame-major (GMM_HOST_FRAME_MAJOR, the
+    drop-in's own table layout)."""
     import rasr_amd as ra
     fpl = args.frames or FRAMES_PER_LAUNCH
     sc = ra.Scorer(ms, kind, max_frames=fpl)
@@ -468,8 +474,8 @@ def host_boundary(args, ms, kind, calls=6):
     out_fm = ra.pinned_empty((fpl, m), "float32")
     legs = {
         "scores_and_best": (lambda: sc.score_host(frames, out=out, best_out=best), 8),
-        "scores_only": (lambda: sc.score_host_ring(frames, 0, fpl, out, keep_best=True), 4),
-        "scores_only_frame_major": (lambda: sc.score_host_ring(frames, 0, fpl, out_fm, keep_best=True,
+        "scores_only": (lambda: sc.score_host_ring(frames, 0, fpl, out, lazy_best=True), 4),
+        "scores_only_frame_major": (lambda: sc.score_host_ring(frames, 0, fpl, out_fm, lazy_best=True,
                                                                 frame_major=True), 4),
     }
     rec = {"unit": "frames/s", "scorer": kind, "frames_per_call": fpl,
@@ -497,11 +503,11 @@ def host_leg_all_ranks(args, ms, kind, ws, rank, local, calls=6):
     sc = ra.Scorer(ms, kind, max_frames=fpl, device=local)
     frames = ra.synthetic_frames(fpl, args.dim, seed=555 + rank)
     out = ra.pinned_empty((sc.n_mixtures(), fpl), "float32")
-    sc.score_host_ring(frames, 0, fpl, out, keep_best=True)  # warm-up
+    sc.score_host_ring(frames, 0, fpl, out, lazy_best=True)  # warm-up
     barrier(ws)
     t0 = time.perf_counter()
     for _ in range(calls):
-        sc.score_host_ring(frames, 0, fpl, out, keep_best=True)
+        sc.score_host_ring(frames, 0, fpl, out, lazy_best=True)
     dt = time.perf_counter() - t0
     barrier(ws)
     sc.close()
@@ -779,7 +785,7 @@ def main():
     extra = {}
     if not args.no_extra_mode:
         # the other headline-model scorers (nn returned above): fp32 / SIMD, and the batched int scorer
-        for other in [m for m in ("fp32", "simd", "bint") if m != args.mode]:
+        for other in [m for m in ("fp32", "simd", "bint", "simd-scores", "fp32-scores") if m != args.mode]:
             r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_LAUNCHES[other])
             extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
                             "frames_per_gpu_per_step": r2["frames_per_step"],
@@ -829,7 +835,8 @@ def main():
                 "dimension": args.dim,
                 "frames_per_gpu_per_step": res["frames_per_step"],
                 "frames_per_launch": res["frames_per_launch"],
-                "best_density": not args.no_best and not args.mode.startswith("presel") and args.mode != "bint",
+                "best_density": not (args.no_best or args.mode.startswith("presel") or args.mode == "bint"
+                                     or args.mode.endswith("-scores")),
                 "parallelism": (f"mixture-sharded x{ws} + RCCL all-gather" if args.parallel == "mixtures" and ws > 1
                                 else f"density-sharded x{ws} + RCCL all-reduce(MIN) of split mixtures + all-gather"
                                 if args.parallel == "densities" and ws > 1 else f"frame-sharded replicas x{ws}"),

@@ -165,11 +165,19 @@ int gmm_score_host(gmm_scorer* scorer, const float* frames, uint32_t n_frames, u
  * *call_id (may be NULL) receives the call's id. */
 #define GMM_HOST_KEEP_BEST 1u
 #define GMM_HOST_FRAME_MAJOR 2u
+/* flags: GMM_HOST_LAZY_BEST (best_density must be NULL; not with GMM_HOST_KEEP_BEST): the call computes scores
+ *   only -- SIMD-diagonal-maximum on its score-only kernel, the float types without the index tag, so their
+ *   scores are plain f32 -- and keeps its frames on the device until the scorer's next host call;
+ *   gmm_fetch_best_density then computes the best densities from them (one more scoring pass over the call's
+ *   frames, whose scores are not copied again).  The reference likewise evaluates bestDensity(e) only when
+ *   asked (AssigningFeatureScorer.hh:110-121): a search that reads only score(e) never pays for the
+ *   assignment. */
+#define GMM_HOST_LAZY_BEST 4u
 int gmm_score_host_ring(gmm_scorer* scorer, const float* ring, uint32_t ring_size, uint32_t first,
                         uint32_t n_frames, uint32_t frame_stride, float* scores, uint32_t* best_density,
                         uint32_t score_stride, uint32_t flags, uint64_t* call_id);
 
-/* Best densities of host call `call_id` (made with GMM_HOST_KEEP_BEST) into the same ring positions of
+/* Best densities of host call `call_id` (made with GMM_HOST_KEEP_BEST or GMM_HOST_LAZY_BEST) into the same ring positions of
  * best_density, in the same layout, that its scores went to.  GMM_ERR_INVALID_ARGUMENT once a later
  * host call of this scorer has replaced them (the caller scores those frames again). */
 int gmm_fetch_best_density(gmm_scorer* scorer, uint64_t call_id, uint32_t* best_density, uint32_t score_stride);

@@ -91,6 +91,7 @@ class EstimatorConfig(ctypes.Structure):
 
 GMM_HOST_KEEP_BEST = 1
 GMM_HOST_FRAME_MAJOR = 2
+GMM_HOST_LAZY_BEST = 4
 # gmm_scorer_create_sharded: the per-frame reduce of mixtures split between GPUs
 GMM_EXCHANGE = {"auto": 0, "rccl": 1, "copy": 2}
 

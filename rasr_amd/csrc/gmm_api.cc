@@ -161,6 +161,7 @@ struct gmm_scorer {
     HostRing                 keptRing{};
     std::vector<HostSegment> keptSegs;
     bool                     keptFrameMajor = false;
+    bool                     keptLazy = false, keptComputed = false;  // GMM_HOST_LAZY_BEST: computed on fetch
     float*                   dHostScoresT   = nullptr;  // frame-major copies (GMM_HOST_FRAME_MAJOR)
     uint32_t*                dHostBestT     = nullptr;
     // kernel timing (gmm_scorer_set_timing)
@@ -170,6 +171,10 @@ struct gmm_scorer {
     // density-sharded handle (gmm_scorer_create_sharded): no model of its own; the parts score, this handle
     // holds the full-table host staging on devices[0]
     std::unique_ptr<DensityGroup, DensityGroupDelete> group;
+    // SIMD-diagonal-maximum: the same model on the score-only class layout, which every call without a best
+    // density table runs (gmm_score_device with best_density NULL, GMM_HOST_LAZY_BEST host calls): the
+    // reference's score(e) without the index-carrying pack, bit-identical scores
+    std::unique_ptr<gmm_scorer> scoresOnly;
 
     ~gmm_scorer() {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
@@ -309,6 +314,8 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
     GMM_HIP_CHECK(hipSetDevice(s->device));
     if (s->group)
         return groupScore(s, frames, nFrames, frameStride, scores, best, scoreStride, stream);
+    if (!best && s->scoresOnly)
+        return scoreImpl(s->scoresOnly.get(), frames, nFrames, frameStride, scores, nullptr, scoreStride, stream);
     const uint32_t fpb         = framesPerBlock(s);
     const uint32_t nFrameTiles = (nFrames + fpb - 1) / fpb;
     const uint32_t nPadCall    = nFrameTiles * fpb;  // rows the scorer reads
@@ -684,7 +691,7 @@ int transposeChunk(gmm_scorer* s, bool scores, bool best, uint32_t t0, uint32_t 
 }
 
 int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, uint32_t scoreStride, bool keepBest,
-                  bool frameMajor) {
+                  bool lazyBest, bool frameMajor) {
     const uint32_t fpb = framesPerBlock(s), nFrames = r.nFrames;
     // frame chunks for large tables; one chunk for preselection (gmm_scorer_cluster_selection reports the
     // last call's whole batch)
@@ -708,7 +715,7 @@ int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* bes
                                        r.frames + static_cast<size_t>(g.col) * r.frameStride,
                                        static_cast<size_t>(r.frameStride) * sizeof(float), D * sizeof(float), g.n,
                                        hipMemcpyHostToDevice, s->hostCompute));
-    const bool withBest = best || keepBest;
+    const bool withBest = best || (keepBest && !lazyBest);
     for (uint32_t k = 0; k < nChunks; ++k) {
         const uint32_t t0 = k * per, n = std::min(per, nFrames - t0);
         rc = scoreImpl(s, s->dHostFrames + t0 * D, n, s->D, s->dHostScores + t0, withBest ? s->dHostBest + t0 : nullptr,
@@ -727,6 +734,8 @@ int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* bes
         s->keptRing      = r;
         s->keptSegs      = segs;
         s->keptFrameMajor = frameMajor;
+        s->keptLazy       = lazyBest;
+        s->keptComputed   = !lazyBest;
     }
     return GMM_OK;
 }
@@ -743,12 +752,16 @@ int scoreHost(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, u
               uint64_t* callId) {
     if (!s)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
-    if ((flags & ~(GMM_HOST_KEEP_BEST | GMM_HOST_FRAME_MAJOR)) != 0)
+    if ((flags & ~(GMM_HOST_KEEP_BEST | GMM_HOST_FRAME_MAJOR | GMM_HOST_LAZY_BEST)) != 0)
         return fail(GMM_ERR_INVALID_ARGUMENT, "unknown flags");
     const bool frameMajor = (flags & GMM_HOST_FRAME_MAJOR) != 0;
-    if ((flags & GMM_HOST_KEEP_BEST) && best)
-        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST with a best_density table");
-    const bool keepBest = (flags & GMM_HOST_KEEP_BEST) && hasAssignment(s);  // batch types: nothing to keep
+    if ((flags & GMM_HOST_KEEP_BEST) && (flags & GMM_HOST_LAZY_BEST))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST and GMM_HOST_LAZY_BEST together");
+    if ((flags & (GMM_HOST_KEEP_BEST | GMM_HOST_LAZY_BEST)) && best)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST / GMM_HOST_LAZY_BEST with a best_density table");
+    // batch types: nothing to keep
+    const bool keepBest = (flags & (GMM_HOST_KEEP_BEST | GMM_HOST_LAZY_BEST)) && hasAssignment(s);
+    const bool lazyBest = keepBest && (flags & GMM_HOST_LAZY_BEST);
     // a new host call replaces the best densities a previous one kept
     s->keptBestCall = 0;
     const uint64_t id = ++s->hostCall;
@@ -772,7 +785,7 @@ int scoreHost(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, u
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostScoresT), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(float)));
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostBestT), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(uint32_t)));
     }
-    const int rc = scoreHostImpl(s, r, scores, best, scoreStride, keepBest, frameMajor);
+    const int rc = scoreHostImpl(s, r, scores, best, scoreStride, keepBest, lazyBest, frameMajor);
     if (rc != GMM_OK)
         for (hipStream_t st : {s->hostCompute, s->hostCopy})
             if (st)
@@ -973,10 +986,12 @@ void DensityGroupDelete::operator()(DensityGroup* g) const {
 namespace {
 }  // namespace
 
-extern "C" {
+namespace {
 
-int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scorer_config* config,
-                      int device, gmm_scorer** out) {
+// classLayout: lay the quantized model out for the score-only kernel (gmm_prepare.cc buildClassLayout) whatever
+// the type (the SIMD scorer's scoresOnly twin); batch-int/-fast use it by default
+int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scorer_config* config, int device,
+                 bool classLayout, gmm_scorer** out) {
     if (!ms || !out)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
@@ -1034,7 +1049,8 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     if (quantized) {
         PreparedQuantized p;
         // batch types have no best densities: the score-only class layout where it applies
-        const bool        scoreOnlyLayout = !presel && flavor == Flavor::BatchInt && !(cfg.flags & GMM_FLAG_FULL_KEYS);
+        const bool        scoreOnlyLayout =
+                classLayout || (!presel && flavor == Flavor::BatchInt && !(cfg.flags & GMM_FLAG_FULL_KEYS));
         std::string       err = prepareQuantized(*ms, flavor, shard, p, scoreOnlyLayout);
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
@@ -1164,6 +1180,31 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     s->mixBase = shard.begin == 0 && shard.end == 0 ? 0 : shard.begin;
     GMM_HIP_CHECK(hipDeviceSynchronize());
     *out = s.release();
+    return GMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scorer_config* config,
+                      int device, gmm_scorer** out) {
+    int rc = createScorer(ms, type, config, device, false, out);
+    if (rc != GMM_OK || type != GMM_SIMD_DIAGONAL_MAXIMUM || ((*out)->cfg.flags & GMM_FLAG_FULL_KEYS))
+        return rc;
+    gmm_scorer* s = *out;
+    if (s->multiCov || s->kSteps != 1)
+        return GMM_OK;  // the class layout covers one covariance and D <= 64 (the key layout serves the rest)
+    gmm_scorer* twin = nullptr;
+    if ((rc = createScorer(ms, type, &s->cfg, device, true, &twin)) != GMM_OK) {
+        gmm_scorer_destroy(s);
+        *out = nullptr;
+        return rc;
+    }
+    if (twin->scoreOnly)
+        s->scoresOnly.reset(twin);
+    else  // some row's |2 dot + Q| may leave the class layout's range
+        gmm_scorer_destroy(twin);
     return GMM_OK;
 }
 
@@ -1378,6 +1419,20 @@ int gmm_fetch_best_density(gmm_scorer* s, uint64_t callId, uint32_t* best, uint3
         return fail(GMM_ERR_INVALID_ARGUMENT, "score_stride below the call's table layout");
     GMM_HIP_CHECK(hipSetDevice(s->device));
     int rc = GMM_OK;
+    if (!s->keptComputed) {
+        // GMM_HOST_LAZY_BEST: score the call's frames (still in dHostFrames) again, with best densities, in one
+        // launch; its scores land in the device table only (the caller's copy stays the score-only one)
+        const uint32_t n = s->keptRing.nFrames;
+        rc = scoreImpl(s, s->dHostFrames, n, s->D, s->dHostScores, s->dHostBest, n, s->hostCompute);
+        if (rc != GMM_OK) {
+            (void)hipStreamSynchronize(s->hostCompute);
+            return rc;
+        }
+        if (!s->keptFrameMajor)
+            for (const HostSegment& g : s->keptSegs)
+                GMM_HIP_CHECK(hipEventRecord(s->chunkDone[g.chunk], s->hostCompute));
+        s->keptComputed = true;
+    }
     if (s->keptFrameMajor) {  // transpose the kept best densities now; every chunk's copy waits for it
         if ((rc = transposeChunk(s, false, true, 0, s->keptRing.nFrames, s->keptRing.nFrames)) != GMM_OK)
             return rc;
@@ -1481,6 +1536,8 @@ int gmm_scorer_set_timing(gmm_scorer* s, int enable) {
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
     s->timing     = enable != 0;
     s->eventsUsed = 0;
+    if (s->scoresOnly)
+        gmm_scorer_set_timing(s->scoresOnly.get(), enable);
     if (s->group)  // sharded: every part times its own kernels
         for (DensityPart& p : s->group->parts)
             if (p.scorer)
@@ -1517,10 +1574,20 @@ int gmm_scorer_kernel_time(gmm_scorer* s, double* totalMs, uint32_t* nLaunches, 
         GMM_HIP_CHECK(hipEventElapsedTime(&ms, s->events[i].first, s->events[i].second));
         total += ms;
     }
+    uint32_t launches = static_cast<uint32_t>(s->eventsUsed);
+    if (s->scoresOnly) {  // calls without best densities ran on the twin
+        double   t = 0;
+        uint32_t k = 0;
+        int      rc;
+        if ((rc = gmm_scorer_kernel_time(s->scoresOnly.get(), &t, &k, reset)) != GMM_OK)
+            return rc;
+        total += t;
+        launches += k;
+    }
     if (totalMs)
         *totalMs = total;
     if (nLaunches)
-        *nLaunches = static_cast<uint32_t>(s->eventsUsed);
+        *nLaunches = launches;
     if (reset)
         s->eventsUsed = 0;
     return GMM_OK;

@@ -290,7 +290,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     loadTile(T0 + 2, R2, C2);
     loadTile(T0 + 3, R3, C3);
 
-    const uint32_t kmask = (1u << a.tileBits) - 1u;
+    // scores only (no best density, no preselection mask): keys are the values' own bits, nothing masked
+    const uint32_t kmask = (BEST || PRESEL) ? (1u << a.tileBits) - 1u : 0u;
     // the value mask lives in a VGPR so that (bits & mask) | tag is ONE v_and_or_b32 with the tag in an
     // SGPR (gfx950 VOP3 reads at most one SGPR)
     uint32_t vmask = ~kmask;
@@ -347,8 +348,12 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
                     best[cb][r] = umin3(best[cb][r], (__float_as_uint(acc[0][cb][r]) & vmask) | ca,
                                         (__float_as_uint(acc[1][cb][r]) & vmask) | cc);
                 }
-                else {
+                else if constexpr (BEST) {
                     best[cb][r] = umin3(best[cb][r], ka, kb);
+                }
+                else {  // scores only: the full f32 value, no tag (one v_min3_u32 per two values)
+                    (void)ka, (void)kb;
+                    best[cb][r] = umin3(best[cb][r], __float_as_uint(acc[0][cb][r]), __float_as_uint(acc[1][cb][r]));
                 }
             }
     };
@@ -463,7 +468,8 @@ __device__ __forceinline__ void emitMixtureSplit32(const SplitArgs& a, const uin
     // (value, tile) first, then the row in the tile: row(i, h) = (i & 3) + 8 (i >> 2) + 4 h
     const uint32_t hi0  = r[0] & ~15u, hi1 = r[1] & ~15u;
     const uint32_t row0 = (r[0] & 3u) | ((r[0] & 12u) << 1), row1 = ((r[1] & 3u) | ((r[1] & 12u) << 1)) + 4u;
-    const bool     take = hi1 < hi0 || (hi1 == hi0 && row1 < row0);
+    // scores only: untagged values, the plain minimum
+    const bool     take = BEST ? (hi1 < hi0 || (hi1 == hi0 && row1 < row0)) : r[1] < r[0];
     const uint32_t key  = take ? r[1] : r[0];
     const uint32_t row  = take ? row1 : row0;
 
@@ -525,7 +531,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     loadTile(T0, R0);
     loadTile(T0 + 1, R1);
 
-    const uint32_t kmask = (1u << a.tileBits) - 1u;
+    const uint32_t kmask = BEST ? (1u << a.tileBits) - 1u : 0u;  // scores only: untagged values
     uint32_t       vmask = ~kmask;
     asm volatile("" : "+v"(vmask));
     const float noneScore = __fmul_rn(a.outScale, a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f);
@@ -559,6 +565,11 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
+                if constexpr (!BEST) {  // scores only: the values' own bits
+                    best[b][q] = umin3(umin3(best[b][q], __float_as_uint(acc[b][q]), __float_as_uint(acc[b][q + 4])),
+                                       __float_as_uint(acc[b][q + 8]), __float_as_uint(acc[b][q + 12]));
+                    continue;
+                }
                 const uint32_t k0 = (__float_as_uint(acc[b][q]) & vmask) | tag[q];
                 const uint32_t k1 = (__float_as_uint(acc[b][q + 4]) & vmask) | tag[q + 4];
                 const uint32_t k2 = (__float_as_uint(acc[b][q + 8]) & vmask) | tag[q + 8];

@@ -240,6 +240,7 @@ struct GpuFeatureScorer::Slot {
     HostTable<float>    scores;  // [nMixtures]
     HostTable<uint32_t> best;    // [nMixtures]
     std::vector<float>  frame;   // the frame, for scoring it again
+    std::vector<float>  scratch; // scores of that second scoring (the context keeps its first ones)
     uint64_t            call = 0;
     bool                bestValid = false;
 };
@@ -284,7 +285,7 @@ Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
     slot->frame.assign(f.begin(), f.end());
     ++launches_;
     if (gmm_score_host_ring(handle_, slot->frame.data(), 1, 0, 1, dimension_, slot->scores.data(), nullptr, 1,
-                            assigning_ ? GMM_HOST_KEEP_BEST : 0u, &slot->call) != GMM_OK)
+                            assigning_ ? GMM_HOST_LAZY_BEST : 0u, &slot->call) != GMM_OK)
         criticalError("gmm_score_host_ring");
     slot->bestValid = false;
     return std::make_shared<FrameScorer>(this, std::move(slot), pool_, nMixtures_, assigning_);
@@ -292,13 +293,15 @@ Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
 
 DensityInMixture GpuFeatureScorer::slotBestDensity(Slot& slot, EmissionIndex e) const {
     if (!slot.bestValid) {
-        // the device still holds them if no later frame was scored; otherwise score this frame again
-        // (bit-identical scores, its best densities copied directly)
+        // computed from the frame the device still holds if no later frame was scored; otherwise score this
+        // frame again, its best densities copied directly (its scores into scratch: the float types' keyed
+        // scores carry fewer bits, and the context's scores stay the ones it already returned)
         if (gmm_fetch_best_density(handle_, slot.call, slot.best.data(), 1) == GMM_OK)
             ++bestFetches_;
         else {
             ++launches_;
-            if (gmm_score_host(handle_, slot.frame.data(), 1, dimension_, slot.scores.data(), slot.best.data(), 1) != GMM_OK)
+            slot.scratch.resize(std::max<uint32_t>(nMixtures_, 1));
+            if (gmm_score_host(handle_, slot.frame.data(), 1, dimension_, slot.scratch.data(), slot.best.data(), 1) != GMM_OK)
                 criticalError("gmm_score_host");
         }
         slot.bestValid = true;
@@ -383,7 +386,7 @@ void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
     uint64_t       call = 0;
     ++launches_;
     if (gmm_score_host_ring(handle_, features_.data(), b, p, length, dimension_, scores_.data(), nullptr, rowStride(),
-                            GMM_HOST_FRAME_MAJOR | (assigning_ ? GMM_HOST_KEEP_BEST : 0u), &call) != GMM_OK)
+                            GMM_HOST_FRAME_MAJOR | (assigning_ ? GMM_HOST_LAZY_BEST : 0u), &call) != GMM_OK)
         criticalError("gmm_score_host_ring");
     for (uint32_t i = 0; i < length; ++i) {
         const uint32_t q = (p + i) % b;
@@ -418,12 +421,15 @@ DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t
                     bestCached_[q] = 1;
         }
         else {
-            // a later fill replaced them on the device: score this position again (its row of features_ is
-            // unchanged while cached_[p] holds), best densities copied directly
+            // a later fill replaced its frames on the device: score this position again (its row of features_
+            // is unchanged while cached_[p] holds), best densities copied directly into its row of best_, the
+            // scores into scratch (the row of scores_ keeps the score-only values it already returned)
             uint64_t again = 0;
             ++launches_;
-            if (gmm_score_host_ring(handle_, features_.data(), bufferSize_, p, 1, dimension_, scores_.data(), best_.data(),
-                                    rowStride(), GMM_HOST_FRAME_MAJOR, &again) != GMM_OK)
+            scratch_.resize(rowStride());
+            if (gmm_score_host_ring(handle_, features_.data() + static_cast<size_t>(p) * dimension_, 1, 0, 1, dimension_,
+                                    scratch_.data(), best_.data() + static_cast<size_t>(p) * rowStride(), rowStride(),
+                                    GMM_HOST_FRAME_MAJOR, &again) != GMM_OK)
                 criticalError("gmm_score_host_ring");
             bestCall_[p] = again;
         }

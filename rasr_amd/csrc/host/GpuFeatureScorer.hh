@@ -172,8 +172,8 @@ protected:
 // Unbuffered scorer: every getScorer() scores one frame against all mixtures on the GPU
 // (the SIMD / diagonal-maximum scorers' Context, SimdFeatureScorer.cc:22-35).  The contexts' tables are
 // page-locked slots recycled when the caller drops a context (no allocation per frame); best densities
-// stay on the device until bestDensity() asks for them (gmm_fetch_best_density), or -- after a later
-// frame replaced them there -- that frame is scored again.  Contexts refer to their scorer, which must
+// are computed only when bestDensity() asks for them (GMM_HOST_LAZY_BEST + gmm_fetch_best_density from the
+// frame still on the device), or -- after a later frame replaced it there -- that frame is scored again.  Contexts refer to their scorer, which must
 // outlive them (as the reference's Context refers to its featureScorer_, SimdFeatureScorer.hh:51-68).
 class GpuFeatureScorer : public FeatureScorer {
 public:
@@ -233,11 +233,13 @@ private:
     // positions, wrapped or not, whose frames and score rows move by DMA directly.  The tables are
     // frame-major, [bufferSize][nMixtures] (the reference's scores_ is [nMixtures][bufferSize],
     // BatchFeatureScorer.hh:177-186, filled one mixture at a time): a context's score(e) calls walk one
-    // contiguous row instead of one cache line per emission.  Best densities (assigning types) stay on
-    // the device until bestDensity() asks for them: a score-only caller moves 4 B per (frame, mixture), not 8.
+    // contiguous row instead of one cache line per emission.  Best densities (assigning types) are
+    // computed only when bestDensity() asks for them (GMM_HOST_LAZY_BEST): a score-only caller runs the
+    // score-only kernels and moves 4 B per (frame, mixture), not 8.
     HostTable<float>          features_;
     HostTable<float>          scores_;
     HostTable<uint32_t>       best_;
+    mutable std::vector<float> scratch_;     // [nMixtures] scores of a re-scored position (not kept)
     mutable std::vector<char> cached_;       // [bufferSize] scores of the position are in scores_
     mutable std::vector<char> bestCached_;   // [bufferSize] best densities of the position are in best_
     mutable std::vector<uint64_t> bestCall_; // [bufferSize] host call that scored the position

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-3 session 8: score-only paths (SIMD twin on the class layout, untagged float epilogue, GMM_HOST_LAZY_BEST):
+# GPU tests, smoke, and a bench line with the -scores modes (no CPU baseline, no extras).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${RUN:-r03_s8}
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>; ALLOW_FAIL=1: a plain failure (rc 1: failed tests) does not stop the run
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -3 $OUT/$name.log
+  if [ $rc -eq 1 ] && [ -n "$ALLOW_FAIL" ]; then return 0; fi
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+ALLOW_FAIL=1 step pytest_new 400 python -u -m pytest tests/test_scores_only.py tests/test_host_pipeline.py -q -m gpu --timeout 120 --timeout-method thread
+ALLOW_FAIL=1 step pytest 1100 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 900 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off --extras off --host-boundary off
+echo done

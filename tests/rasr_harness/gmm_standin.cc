@@ -143,11 +143,14 @@ int gmm_score_host_ring(gmm_scorer* s, const float* ring, uint32_t R, uint32_t f
                         float* scores, uint32_t* best, uint32_t stride, uint32_t flags, uint64_t* callId) {
     if (!s)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
-    if ((flags & GMM_HOST_KEEP_BEST) && best)
-        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST with a best_density table");
+    if ((flags & GMM_HOST_KEEP_BEST) && (flags & GMM_HOST_LAZY_BEST))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST and GMM_HOST_LAZY_BEST together");
+    if ((flags & (GMM_HOST_KEEP_BEST | GMM_HOST_LAZY_BEST)) && best)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST / GMM_HOST_LAZY_BEST with a best_density table");
     const bool fm       = (flags & GMM_HOST_FRAME_MAJOR) != 0;
     const bool assign   = s->type == GMM_SIMD_DIAGONAL_MAXIMUM || s->type == GMM_DIAGONAL_MAXIMUM;
-    const bool keepBest = (flags & GMM_HOST_KEEP_BEST) && assign;
+    // the stand-in computes the best densities with the scores either way (the oracle has no score-only mode)
+    const bool keepBest = (flags & (GMM_HOST_KEEP_BEST | GMM_HOST_LAZY_BEST)) && assign;
     s->keptCall         = 0;
     const uint64_t id   = ++s->call;
     if (callId)

@@ -117,6 +117,9 @@ def test_pinned_empty_roundtrip(built):
 
 
 def _ring_case(sc, ring, first, n, pinned, keep_best, frame_major=False):
+    """keep_best: False (best densities copied with the scores), True (GMM_HOST_KEEP_BEST: computed, fetched
+    later) or "lazy" (GMM_HOST_LAZY_BEST: scores only, computed when fetched -- its scores are those of a
+    device call without best densities)."""
     m = sc.n_mixtures()
     R = ring.shape[0]
     mk = (lambda shape, dt: ra.pinned_empty(shape, dt)) if pinned else (lambda shape, dt: np.empty(shape, dt))
@@ -126,8 +129,11 @@ def _ring_case(sc, ring, first, n, pinned, keep_best, frame_major=False):
     best[:] = 123456
     order = [(first + i) % R for i in range(n)]
     ref_s, ref_b = _device_reference(sc, np.ascontiguousarray(ring[order]), True)
-    cid = sc.score_host_ring(ring, first, n, out, None if keep_best else best, keep_best=keep_best,
-                             frame_major=frame_major)
+    lazy = keep_best == "lazy"
+    if lazy:
+        ref_s, _ = _device_reference(sc, np.ascontiguousarray(ring[order]), False)
+    cid = sc.score_host_ring(ring, first, n, out, None if keep_best else best, keep_best=keep_best is True,
+                             frame_major=frame_major, lazy_best=lazy)
     if keep_best:
         assert (best == 123456).all()  # nothing copied yet
         sc.fetch_best(cid, best)
@@ -150,7 +156,7 @@ def _ring_case(sc, ring, first, n, pinned, keep_best, frame_major=False):
 @pytest.mark.parametrize("R,first,n", [(7, 5, 6), (7, 0, 7), (64, 63, 2), (64, 10, 30), (9000, 8000, 9000),
                                        (20000, 3, 17000)])
 @pytest.mark.parametrize("pinned", [False, True])
-@pytest.mark.parametrize("keep_best", [False, True])
+@pytest.mark.parametrize("keep_best", [False, True, "lazy"])
 @pytest.mark.parametrize("frame_major", [False, True])
 def test_ring_matches_device(gpu, model, kind, R, first, n, pinned, keep_best, frame_major):
     """Small (one chunk) and pipelined (several chunks, the wrap inside a chunk) ring calls, pageable and pinned
