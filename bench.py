@@ -590,10 +590,12 @@ def drop_in(args, kind):
     if not os.access(drv, os.X_OK):
         return {"error": f"{drv} not built"}
     recs = []
-    runs = [(DROP_IN_SIZES, DROP_IN_FRAMES, 0), ([4096], [262144], 1)]
-    for sizes, frames, best in runs:
+    # (sizes, frames, read best densities, share of emissions read per frame in permille): the dump consumer at
+    # every size, the aligners' read, and a search-like consumer reading 10 % of the emissions
+    runs = [(DROP_IN_SIZES, DROP_IN_FRAMES, 0, 1000), ([4096], [262144], 1, 1000), ([512, 4096], [196608, 262144], 0, 100)]
+    for sizes, frames, best, permille in runs:
         cmd = [drv, "bench", kind, ",".join(map(str, sizes)), ",".join(map(str, frames)), str(args.mixtures),
-               str(args.densities), str(args.dim), str(best)]
+               str(args.densities), str(args.dim), str(best), str(permille)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         except subprocess.TimeoutExpired:
@@ -601,7 +603,8 @@ def drop_in(args, kind):
         if r.returncode != 0:
             return {"error": f"driver exit {r.returncode}: {r.stderr[-300:]}", "runs": recs}
         recs += [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
-    return {"scorer": kind, "consumer": "score(e) of every emission per frame (FeatureScorerNode dump)",
+    return {"scorer": kind, "consumer": "score(e) of every emission per frame (FeatureScorerNode dump); "
+                                        "read_permille 100: of a scattered 10 % per frame (the search's active states)",
             "runs": [{k: v for k, v in x.items() if k not in ("mixtures", "densities", "dim", "checksum", "type")}
                      for x in recs]}
 

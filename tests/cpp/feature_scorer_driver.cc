@@ -68,10 +68,13 @@ static std::unique_ptr<Mm::Gpu::MixtureSet> readBinaryModel(const std::string& p
 // ---------------------------------------------------------------------------------------------------------
 // bench mode: the drop-in's throughput through the recognizer protocol, PCIe included
 //   feature_scorer_driver bench <type> <bufferSizes> <frames> <mixtures> <densitiesPerMixture> <dim> <best 0|1>
+//                               [readPermille]
 // bufferSizes / frames: comma-separated lists of equal length (one scorer per buffer size, timed on that many
 // frames).  Synthetic model of SURVEY 8(d) (means N(0,1), pooled variance 0.5 + |N(0,1)|, uniform weights;
 // splitmix64 + Box-Muller) and N(0,1) frames.  Every frame's context is consumed as FeatureScorerNode dumps
 // it: score(e) for every emission (and bestDensity(e) for every emission with best = 1, the aligners' read).
+// readPermille < 1000: a search-like consumer instead, score(e) of that share of the emissions per frame, a
+// scattered set that moves from frame to frame (the search's active states; SearchSpace.cc:1613-1659).
 // One warm-up segment, then one timed segment per size; prints one JSON line per size.
 // ---------------------------------------------------------------------------------------------------------
 namespace {
@@ -104,10 +107,12 @@ std::vector<uint32_t> parseList(const char* s) {
 }  // namespace
 
 static int benchMain(int argc, char** argv) {
-    if (argc != 9) {
-        fprintf(stderr, "usage: %s bench type bufferSizes frames mixtures densitiesPerMixture dim best\n", argv[0]);
+    if (argc != 9 && argc != 10) {
+        fprintf(stderr, "usage: %s bench type bufferSizes frames mixtures densitiesPerMixture dim best [readPermille]\n",
+                argv[0]);
         return 2;
     }
+    const uint32_t permille = argc == 10 ? std::min<uint32_t>(1000, atoi(argv[9])) : 1000;
     const std::string           type  = argv[2];
     const std::vector<uint32_t> sizes = parseList(argv[3]), counts = parseList(argv[4]);
     const uint32_t              M = atoi(argv[5]), K = atoi(argv[6]), D = atoi(argv[7]);
@@ -150,11 +155,19 @@ static int benchMain(int argc, char** argv) {
         }
         double   sink  = 0;
         uint64_t sinkB = 0;
+        uint32_t frameNo = 0;
         auto     consume = [&](const Mm::Gpu::Scorer& s) {
             const uint32_t n   = s->nEmissions();
             float          acc = 0;
-            for (uint32_t e = 0; e < n; ++e)
-                acc += s->score(e);
+            if (permille >= 1000)
+                for (uint32_t e = 0; e < n; ++e)
+                    acc += s->score(e);
+            else {  // every emission whose (frame, e) hash falls below the share
+                const uint64_t f = 0x9e3779b97f4a7c15ull * ++frameNo;
+                for (uint32_t e = 0; e < n; ++e)
+                    if (((f ^ (e * 0xbf58476d1ce4e5b9ull)) >> 33) % 1000u < permille)
+                        acc += s->score(e);
+            }
             sink += acc;
             if (readBest && s->hasBestDensity())
                 for (uint32_t e = 0; e < n; ++e)
@@ -185,8 +198,9 @@ static int benchMain(int argc, char** argv) {
         segment(0, F);
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         printf("{\"type\": \"%s\", \"buffer_size\": %u, \"frames\": %u, \"seconds\": %.6f, \"frames_per_s\": %.1f, "
-               "\"launches\": %u, \"best\": %s, \"mixtures\": %u, \"densities\": %u, \"dim\": %u, \"checksum\": %.6e}\n",
-               type.c_str(), B, F, sec, F / sec, lc() - l0, readBest ? "true" : "false", M, M * K, D,
+               "\"launches\": %u, \"best\": %s, \"read_permille\": %u, \"mixtures\": %u, \"densities\": %u, "
+               "\"dim\": %u, \"checksum\": %.6e}\n",
+               type.c_str(), B, F, sec, F / sec, lc() - l0, readBest ? "true" : "false", permille, M, M * K, D,
                sink + double(sinkB));
         fflush(stdout);
     }
