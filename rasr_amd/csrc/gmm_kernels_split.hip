@@ -761,7 +761,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     loadTile(T0 + 2, R2);
     loadTile(T0 + 3, R3);
 
-    const uint32_t kmask = (1u << a.tileBits) - 1u;
+    const uint32_t kmask = BEST ? (1u << a.tileBits) - 1u : 0u;  // scores only: untagged values
     uint32_t       vmask = ~kmask;
     asm volatile("" : "+v"(vmask));
 
@@ -820,13 +820,14 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         bool reb = false;
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb) {
-            const uint32_t k0 = (__float_as_uint(prev[cb][0]) & vmask) | tag[0];
-            const uint32_t k1 = (__float_as_uint(prev[cb][1]) & vmask) | tag[1];
-            const uint32_t k2 = (__float_as_uint(prev[cb][2]) & vmask) | tag[2];
-            const uint32_t k3 = (__float_as_uint(prev[cb][3]) & vmask) | tag[3];
+            // scores only: the minimum serves the re-base test alone, on the values' own bits (no tag)
+            const uint32_t k0 = BEST ? (__float_as_uint(prev[cb][0]) & vmask) | tag[0] : __float_as_uint(prev[cb][0]);
+            const uint32_t k1 = BEST ? (__float_as_uint(prev[cb][1]) & vmask) | tag[1] : __float_as_uint(prev[cb][1]);
+            const uint32_t k2 = BEST ? (__float_as_uint(prev[cb][2]) & vmask) | tag[2] : __float_as_uint(prev[cb][2]);
+            const uint32_t k3 = BEST ? (__float_as_uint(prev[cb][3]) & vmask) | tag[3] : __float_as_uint(prev[cb][3]);
             best[cb][0]       = umin3(best[cb][0], k0, k1);
             best[cb][1]       = umin3(best[cb][1], k2, k3);
-            const float vmin  = __uint_as_float(min(best[cb][0], best[cb][1]) & vmask);
+            const float vmin  = __uint_as_float(BEST ? min(best[cb][0], best[cb][1]) & vmask : min(best[cb][0], best[cb][1]));
             reb               = reb || __builtin_fmaf(vmin, -kap[cb], Rf[cb]) > 64.0f;
         }
         constexpr int kM1 = KH * NF;
@@ -883,7 +884,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             uint32_t k[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                k[r] = (__float_as_uint(prev[cb][r]) & vmask) | ((tl << 2) | static_cast<uint32_t>(r));
+                k[r] = BEST ? (__float_as_uint(prev[cb][r]) & vmask) | ((tl << 2) | static_cast<uint32_t>(r))
+                            : __float_as_uint(prev[cb][r]);
             best[cb][0]      = umin3(best[cb][0], k[0], k[1]);
             best[cb][1]      = umin3(best[cb][1], k[2], k[3]);
             const float vmin = __uint_as_float(min(best[cb][0], best[cb][1]) & vmask);

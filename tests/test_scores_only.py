@@ -194,3 +194,22 @@ def test_lazy_best_batch_type_and_flags(gpu):
         simd.score_host_ring(frames, 0, 32, out, keep_best=True, lazy_best=True)
     with pytest.raises(ra.GmmError):
         simd.score_host_ring(frames, 0, 32, out, np.zeros((20, 32), np.uint32), lazy_best=True)
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[2], CASES[3]])
+def test_diagonal_sum_scores_only(gpu, case):
+    """diagonal-sum without best densities: the running minimum (for the log-sum-exp re-base only) on untagged
+    values; the scores as with best densities, within the float contract of the oracle."""
+    m, k, d, c, w, f = case
+    ms = ra.synthetic_mixture_set(m, _counts(m, k), d, seed=51 + m, n_covariances=c, weights=w)
+    frames = ra.synthetic_frames(f, d, seed=52)
+    ref = oracle.OracleFloatSum(ms).score(frames, n_threads=8)[0]
+    sc = ra.Scorer(ms, "diagonal-sum", max_frames=f)
+    s, _ = sc.score_host(frames, want_best=False)
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(s), fin)
+    err = np.abs(s.astype(np.float64) - ref)[fin] / np.maximum(1.0, np.abs(ref[fin].astype(np.float64)))
+    assert err.max() <= REL_TOL, f"max rel err {err.max()}"
+    sk, _ = sc.score_host(frames)
+    err2 = np.abs(sk.astype(np.float64) - s)[fin] / np.maximum(1.0, np.abs(s[fin].astype(np.float64)))
+    assert err2.max() <= 1e-5, f"with vs without best densities {err2.max()}"
