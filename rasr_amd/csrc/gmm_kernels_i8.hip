@@ -344,11 +344,14 @@ extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 #define GMM_I8_WAVES 4  // scoreI8Seg, one K step: waves per SIMD the register allocation must allow (0 = free)
 #endif
 //
-// SCORE_ONLY (batch types on the class layout, gmm_prepare.cc buildClassLayout): the row constant h = Q >> 1 is
-// the MFMA's C input, so the accumulator holds v = dot + h and the running minimum is one v_min3 per two
-// candidates straight on the accumulators (no pack: there is no density index to carry).  All rows of a lane
-// group have the same parity p of Q within a mixture (bit g of mixOddMask[m]), so the lane's minimum of
-// 2 dot + Q is 2 min(v) + p, formed once per mixture before the cross-lane reduce.
+// SCORE_ONLY (calls without best densities on the class layout, gmm_prepare.cc buildClassLayout): the row
+// constant h = Q >> 1 is the MFMA's C input, so the accumulator holds v = dot + h (no pack: there is no density
+// index to carry).  A mixture's class tiles come first: all their rows in lane group g have the parity p_g of Q
+// (bit g of the mixture word mixOddMask[m]), so the running minimum there is one v_min3 per two candidates
+// straight on the accumulators, and the lane's minimum of 2 dot + Q is 2 min(v) + p_g.  Its mixed tiles follow
+// (word bits 16-31: the class tile count; bits 4-15: er): row 4g + r of mixed tile i has parity
+// (16 i + 4g + r >= er), and their candidates 2 v + p go to a second running minimum, merged at the mixture end.
+// A pair step holds two tiles of one kind.
 template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles, bool SCORE_ONLY = false>
 __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_WAVES : 1) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
                                                    float* __restrict__ scores, uint32_t* __restrict__ bestOut,
@@ -411,8 +414,9 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     };
     {
         int8_t* const dummy = lds + 2 * kSegBytes;
-        // non-PRESEL rows compare signed (INT_MAX never wins), PRESEL rows unsigned (biased: all ones)
-        const uint32_t never = PRESEL ? 0xffffffffu : 0x7fffffffu;
+        // non-PRESEL rows compare signed (INT_MAX never wins), PRESEL rows unsigned (biased: all ones);
+        // SCORE_ONLY: the class layout's padding value (2 v + 1 of a mixed step stays inside int32)
+        const uint32_t never = PRESEL ? 0xffffffffu : (SCORE_ONLY ? 0x30000000u : 0x7fffffffu);
         for (uint32_t i = threadIdx.x; i < kDummyBytes / 4; i += 256u)
             reinterpret_cast<uint32_t*>(dummy)[i] = (i >= kTileA / 4 && i < kTileA / 4 + 16) ? never : 0u;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before use by the first segment's barrier
@@ -504,28 +508,46 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     // register costs a wait state per link)
     constexpr int kSlots = SCORE_ONLY ? 2 : (KS == 1 ? GMM_I8_SLOTS : 4);
     static_assert(kSlots == 1 || kSlots == 2 || kSlots == 4, "slots");
+    // SCORE_ONLY: minima of v = dot + h over a mixture's class tiles; at its first mixed tile they become 2 v + p_g
+    // in place, and the mixed tiles' 2 v + p join them
     int best[NF][kSlots];
     const auto resetBest = [&]() {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-            for (int r = 0; r < kSlots; ++r)
-                best[cb][r] = PRESEL ? -1 : INT_MAX;  // PRESEL: 0xffffffff = biased INT_MAX
+            for (int r = 0; r < kSlots; ++r)  // PRESEL: 0xffffffff = biased INT_MAX; SCORE_ONLY: 2 v + 1 fits
+                best[cb][r] = PRESEL ? -1 : (SCORE_ONLY ? 0x3fffffff : INT_MAX);
     };
+    // SCORE_ONLY: the class tiles' minima of mixture mm as 2 v + p_g (this lane group's parity there)
+    const auto toMixed = [&](uint32_t mm) {
+        const uint32_t p = (mixOddMask[mm] >> g) & 1u;
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+            for (int r = 0; r < kSlots; ++r)
+                best[cb][r] = static_cast<int>((static_cast<uint32_t>(best[cb][r]) << 1) + p);
+    };
+    uint32_t m    = m0;
+    uint32_t tEnd = mixTileOff[m0 + 1];
+    // SCORE_ONLY: the end of mixture m's class tiles, and its mixed rows' first odd index
+    uint32_t tCls = 0, er = 0;
     // hot: the end of a mixture with tiles (its minimum is a real row: no INT_MAX case, unless PRESEL)
     const auto emit = [&](uint32_t mm, auto hot) {
         constexpr bool kMaybeNone = PRESEL || !decltype(hot)::value;
         if constexpr (SCORE_ONLY) {
             if constexpr (decltype(hot)::value) {
-                // this lane group's parity in mixture mm: the minimum of 2 dot + Q is 2 v + p
-                const int p = (static_cast<int>(mixOddMask[mm]) >> g) & 1;
+                // a mixture without mixed tiles still holds its class minima v: 2 v + p_g (uniform test)
+                if (tCls >= tEnd)
+                    toMixed(mm);
+                emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, 0, ssOut);
+            }
+            else {
+                int none[NF][1];  // a mixture without tiles: Core::Type<int>::max
 #pragma unroll
                 for (int cb = 0; cb < NF; ++cb)
-#pragma unroll
-                    for (int r = 0; r < kSlots; ++r)
-                        best[cb][r] = static_cast<int>((static_cast<uint32_t>(best[cb][r]) << 1) + static_cast<uint32_t>(p));
+                    none[cb][0] = INT_MAX;
+                emitMixtureI8<NF, kMaybeNone, 1>(a, scores, bestOut, none, mm, frame0, lane, g, 0, ssOut);
             }
-            emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, 0, ssOut);
         }
         else if constexpr (PRESEL) {
             int unb[NF][kSlots];
@@ -543,14 +565,22 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     const std::true_type  kHot{};
     const std::false_type kEmpty{};
     resetBest();
-    uint32_t m    = m0;
-    uint32_t tEnd = mixTileOff[m0 + 1];
+    const auto mixWord = [&]() {
+        if constexpr (SCORE_ONLY) {
+            if (m < m1) {
+                const uint32_t w = mixOddMask[m];
+                tCls             = mixTileOff[m] + (w >> 16);
+                er               = (w >> 4) & 0xfffu;
+            }
+        }
+    };
     // mixtures without tiles at the start of the chunk
     while (m < m1 && tEnd == T0) {
         emit(m, kEmpty);
         ++m;
         tEnd = m < m1 ? mixTileOff[m + 1] : T1;
     }
+    mixWord();
 
     for (uint32_t s = 0; s < nSeg; ++s) {
         // this segment's pieces (issued one segment ago) have landed; the next segment's stay in flight
@@ -566,9 +596,10 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         uint32_t       t      = segT0;
         while (t < segEnd) {
             const uint32_t lt = t - segT0;
-            // two tiles of the same mixture, or the last one beside the never-winning stand-in:
-            // 2 NF independent MFMAs, one v_min3 per candidate pair
-            const bool          two   = t + 1 < segEnd && t + 1 < tEnd;  // uniform
+            // two tiles of the same mixture (SCORE_ONLY: of the same kind), or the last one beside the
+            // never-winning stand-in: 2 NF independent MFMAs, one v_min3 per candidate pair
+            const bool          mixed = SCORE_ONLY && t >= tCls;  // uniform
+            const bool          two   = t + 1 < segEnd && t + 1 < tEnd && (!SCORE_ONLY || (t + 1 >= tCls) == mixed);
             const int8_t* const dummy = lds + 2 * kSegBytes;
             const int8_t* const a0    = base + lt * kTileA;
             const int8_t* const a1    = two ? a0 + kTileA : dummy;
@@ -599,6 +630,27 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 for (int ks = 0; ks < KS; ++ks) {
                     accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[ks], B[cb][ks], accA[cb], 0, 0, 0);
                     accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[ks], B[cb][ks], accB[cb], 0, 0, 0);
+                }
+            };
+            // SCORE_ONLY mixed step: the parity of this lane's row r in each tile (row 4g + r of mixed tile i is
+            // remainder entry 16 i + 4g + r, odd from er on; the stand-in's rows never win either way)
+            int        pA[4] = {}, pB[4] = {};
+            const auto parities = [&]() {  // p = (row index >= er) as a sign bit: no compare + select
+                const int thr = static_cast<int>(er) - 16 * static_cast<int>(t - tCls) - 4 * g - 1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    pA[r] = static_cast<int>(static_cast<uint32_t>(thr - r) >> 31);
+                    pB[r] = static_cast<int>(static_cast<uint32_t>(thr - 16 - r) >> 31);
+                }
+            };
+            const auto epilogueMixed = [&](int cb) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ua = static_cast<int>((static_cast<uint32_t>(accA[cb][r]) << 1) + static_cast<uint32_t>(pA[r]));
+                    const int ub = static_cast<int>((static_cast<uint32_t>(accB[cb][r]) << 1) + static_cast<uint32_t>(pB[r]));
+                    int&      bs = best[cb][r % kSlots];
+                    bs           = min(bs, min(ua, ub));
+                    asm volatile("" : "+v"(bs));
                 }
             };
             const auto epilogue = [&](int cb) {
@@ -634,8 +686,8 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             // SCORE_ONLY: the epilogue is 4 v_min3 per block, too short to cover the MFMA latency at lag 1; lag 3
             // leaves the compiler the fewest hazard waits (A/B, 32768 frames: lag 3 1.338 ms, lag 2 1.341, a
             // separate single-tile step for odd tile counts 1.362)
-            constexpr int kLag = SCORE_ONLY ? 3 : 1;
-            {
+            const auto pipeline = [&](auto lagC, auto epi) {
+                constexpr int kLag = decltype(lagC)::value;
 #pragma unroll
                 for (int cb = 0; cb < kLag; ++cb)
                     mfmas(cb);
@@ -643,7 +695,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 for (int cb = kLag; cb < NF; ++cb) {
                     __builtin_amdgcn_sched_barrier(0);
                     mfmas(cb);
-                    epilogue(cb - kLag);
+                    epi(cb - kLag);
                     // inside the chunk: the MFMAs first, then the epilogue (the scheduler would lead with the VALU)
                     __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);
                     __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);
@@ -651,8 +703,20 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int cb = NF - kLag; cb < NF; ++cb)
-                    epilogue(cb);
+                    epi(cb);
+            };
+            if constexpr (SCORE_ONLY) {
+                if (mixed) {  // uniform; a few tiles per mixture: the key layout's lag
+                    if (t == tCls)  // the mixture's first mixed tile
+                        toMixed(m);
+                    parities();
+                    pipeline(std::integral_constant<int, 1>{}, epilogueMixed);
+                }
+                else
+                    pipeline(std::integral_constant<int, 3>{}, epilogue);
             }
+            else
+                pipeline(std::integral_constant<int, 1>{}, epilogue);
             t += two ? 2u : 1u;
             // the mixture ending here, and further ones without tiles ending at the same point (rare)
             if (t == tEnd && m < m1) {
@@ -665,6 +729,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                     ++m;
                     tEnd = m < m1 ? mixTileOff[m + 1] : T1;
                 }
+                mixWord();
             }
         }
         __builtin_amdgcn_sched_barrier(0);

@@ -173,16 +173,27 @@ static ShardRange normalizeShard(const gmm_mixture_set& ms, ShardRange s) {
 // quantized scorers: SIMD-diagonal-maximum, batch-diagonal-maximum-int
 // ---------------------------------------------------------------------------
 
-// Score-only class layout (PreparedQuantized::scoreOnly).  Per mixture, the entries with even and odd
-// Q = c + sum a'^2 go to disjoint lane groups of its tiles (ke groups even, 4 - ke odd, ke chosen for the
-// fewest tiles); a row carries h = Q >> 1 (the MFMA's C input) and -a' as before.  Padding rows carry
-// kClassPadC (never below a real row's v = dot + h, and 2 v + 1 stays inside int32).
+// Score-only class layout (PreparedQuantized::scoreOnly).  A mixture's tiles are `nc` class tiles followed by
+// mixed tiles.  In a class tile the entries with even and odd Q = c + sum a'^2 sit in disjoint lane groups (k
+// groups even, 4 - k odd, the same k for all class tiles of the mixture: lane group g's parity is bit g of the
+// mixture's word), so the kernel keeps min(dot + h) there with one v_min3 per two candidates.  The entries the
+// class tiles leave over go to the mixed tiles, evens first, in row order (row 4g + r of mixed tile i is entry
+// 16 i + 4g + r of that remainder, odd from index `er` on), where the kernel forms 2 (dot + h) + p per candidate.
+// (k, nc) minimise the cost of the mixture's pair steps (a pair step never mixes a class and a mixed tile; an
+// odd count ends on the never-winning stand-in tile), a mixed step counted kMixedCost class steps.  Every row
+// carries h = Q >> 1 (the MFMA's C input) and -a'.  Padding rows carry kClassPadC (never below a real row's
+// value, and 2 v + 1 stays inside int32).  Word of mixture m: bits 0-3 the odd lane groups of its class
+// tiles, bits 4-15 er, bits 16-31 nc.
 static constexpr int32_t kClassPadC  = 0x30000000;
 static constexpr int64_t kClassLimit = int64_t(1) << 29;  // |2 dot + Q| bound of a real row
+static constexpr double  kMixedCost  = 1.25;               // a mixed pair step against a class pair step
 
 // false: some row's |2 dot + Q| may reach kClassLimit; the key layout is used instead
 static bool classLayoutFits(const gmm_mixture_set& ms, ShardRange shard, const PreparedQuantized& out) {
     const uint32_t D = out.dimension, Dp = out.paddedDimension;
+    for (uint32_t m = shard.begin; m < shard.end; ++m)
+        if (ms.mixture_offsets[m + 1] - ms.mixture_offsets[m] > 16u * 65535u)
+            return false;  // the class tile count needs 16 bits of the mixture word
     for (uint32_t x = ms.mixture_offsets[shard.begin]; x < ms.mixture_offsets[shard.end]; ++x) {
         const uint8_t* pm    = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
         int64_t        sumSq = 0, sumAbs = 0;
@@ -200,6 +211,29 @@ static bool classLayoutFits(const gmm_mixture_set& ms, ShardRange shard, const P
     return true;
 }
 
+// the (k, nc) of a mixture with nE even and nO odd entries (ClassPlan::er: even entries left for mixed tiles)
+struct ClassPlan {
+    uint32_t k = 2, nc = 0, nm = 0, er = 0;
+};
+
+static ClassPlan planClassTiles(uint32_t nE, uint32_t nO) {
+    ClassPlan best;
+    double    bestCost = 1e300;
+    for (uint32_t k = 0; k <= 4; ++k) {
+        const uint32_t ce = 4 * k, co = 4 * (4 - k);
+        // class tiles beyond the point where both classes are used up only add padding
+        const uint32_t ncMax = std::max(ce ? (nE + ce - 1) / ce : 0u, co ? (nO + co - 1) / co : 0u);
+        for (uint32_t nc = 0; nc <= ncMax; ++nc) {
+            const uint32_t er = nE - std::min(nE, ce * nc), orr = nO - std::min(nO, co * nc);
+            const uint32_t nm   = (er + orr + 15) / 16;
+            const double   cost = (nc + 1) / 2 + kMixedCost * ((nm + 1) / 2) + 1e-3 * nm;  // ties: fewer mixed tiles
+            if (cost < bestCost)
+                bestCost = cost, best = ClassPlan{k, nc, nm, er};
+        }
+    }
+    return best;
+}
+
 static std::string buildClassLayout(const gmm_mixture_set& ms, ShardRange shard, PreparedQuantized& out) {
     const uint32_t D = out.dimension, Dp = out.paddedDimension, nMix = shard.end - shard.begin;
     Tiling&        t = out.tiling;
@@ -208,36 +242,30 @@ static std::string buildClassLayout(const gmm_mixture_set& ms, ShardRange shard,
     out.mixOddMask.assign(nMix, 0);
     out.tileA.clear();
     out.tileP.clear();
-    std::vector<uint32_t> cls[2];
+    std::vector<uint32_t> cls[2], rest;
     for (uint32_t mi = 0; mi < nMix; ++mi) {
         const uint32_t m = shard.begin + mi;
         const uint32_t b = ms.mixture_offsets[m], e = ms.mixture_offsets[m + 1];
         t.maxEntriesPerMixture = std::max(t.maxEntriesPerMixture, e - b);
         cls[0].clear();
         cls[1].clear();
+        std::vector<int64_t> qOf(e - b);
         for (uint32_t x = b; x < e; ++x) {
             const uint8_t* pm    = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
-            int64_t        sumSq = 0, sumAbs = 0;
+            int64_t        sumSq = 0;
             for (uint32_t k = 0; k < D; ++k) {
                 const int64_t an = 128 - static_cast<int32_t>(pm[k]);
                 sumSq += an * an;
-                sumAbs += an < 0 ? -an : an;
             }
-            (void)sumAbs;  // range checked by classLayoutFits
-            const int64_t q = static_cast<int64_t>(out.constantWeight[x]) + sumSq;
-            cls[static_cast<uint64_t>(q) & 1u].push_back(x);
+            qOf[x - b] = static_cast<int64_t>(out.constantWeight[x]) + sumSq;
+            cls[static_cast<uint64_t>(qOf[x - b]) & 1u].push_back(x);
         }
-        const uint32_t nE = static_cast<uint32_t>(cls[0].size()), nO = static_cast<uint32_t>(cls[1].size());
-        // lane groups for the even class: the fewest tiles (4 rows per lane group per tile)
-        uint32_t ke = nO == 0 ? 4u : (nE == 0 ? 0u : 2u), tiles = UINT32_MAX;
-        for (uint32_t k = (nE ? 1u : 0u); k <= (nO ? 3u : 4u); ++k) {
-            const uint32_t te = k ? (nE + 4 * k - 1) / (4 * k) : 0, to = k < 4 ? (nO + 4 * (4 - k) - 1) / (4 * (4 - k)) : 0;
-            if (std::max(te, to) < tiles)
-                tiles = std::max(te, to), ke = k;
-        }
-        if (nE + nO == 0)
-            tiles = 0;
-        out.mixOddMask[mi] = (0xfu << ke) & 0xfu;
+        const uint32_t  nE = static_cast<uint32_t>(cls[0].size()), nO = static_cast<uint32_t>(cls[1].size());
+        const ClassPlan pl = nE + nO ? planClassTiles(nE, nO) : ClassPlan{2, 0, 0, 0};
+        if (pl.er > 0xfffu || pl.nc > 0xffffu)
+            return "class layout: mixture too large for the mixture word";
+        const uint32_t k = pl.k, tiles = pl.nc + pl.nm;
+        out.mixOddMask[mi] = ((0xfu << k) & 0xfu) | (pl.er << 4) | (pl.nc << 16);
         const uint32_t t0 = t.nTiles;
         t.nTiles += tiles;
         out.tileA.resize(static_cast<size_t>(t.nTiles) * kLanes * 16, 0);
@@ -245,27 +273,33 @@ static std::string buildClassLayout(const gmm_mixture_set& ms, ShardRange shard,
         t.rowEntry.resize(static_cast<size_t>(t.nTiles) * kTileRows, UINT32_MAX);
         t.rowDensityInMixture.resize(static_cast<size_t>(t.nTiles) * kTileRows, UINT32_MAX);
         t.tileCovariance.resize(t.nTiles, 0);
+        const auto place = [&](uint32_t x, uint32_t tile, uint32_t r) {  // row r (4g + j) of tile
+            const uint8_t* pm = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
+            for (uint32_t kk = 0; kk < D; ++kk) {
+                const int32_t  an   = 128 - static_cast<int32_t>(pm[kk]);
+                const uint32_t lane = (kk / 16) * 16 + r, j = kk % 16;  // one K step: kk < 64
+                out.tileA[(static_cast<size_t>(tile) * kLanes + lane) * 16 + j] = static_cast<int8_t>(an);
+            }
+            out.tileP[static_cast<size_t>(tile) * kTileRows + r] = static_cast<int32_t>(qOf[x - b] >> 1);  // floor
+            t.rowEntry[static_cast<size_t>(tile) * kTileRows + r]            = x;
+            t.rowDensityInMixture[static_cast<size_t>(tile) * kTileRows + r] = x - ms.mixture_offsets[shard.begin + mi];
+        };
+        rest.clear();
         for (int c = 0; c < 2; ++c) {
-            const uint32_t g0 = c ? ke : 0, ng = c ? 4 - ke : ke;  // lane groups of the class
+            const uint32_t g0 = c ? k : 0, ng = c ? 4 - k : k;  // lane groups of the class
+            const size_t   cap = static_cast<size_t>(4) * ng * pl.nc;
             for (size_t i = 0; i < cls[c].size(); ++i) {
-                const uint32_t x    = cls[c][i];
+                if (i >= cap) {
+                    rest.push_back(cls[c][i]);  // evens first: c = 0 is placed before c = 1
+                    continue;
+                }
                 const uint32_t tile = t0 + static_cast<uint32_t>(i / (4 * ng));
                 const uint32_t slot = static_cast<uint32_t>(i % (4 * ng));
-                const uint32_t r    = 4 * (g0 + slot / 4) + slot % 4;  // rows 4g..4g+3 belong to lane group g
-                const uint8_t* pm   = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
-                int64_t        sumSq = 0;
-                for (uint32_t k = 0; k < D; ++k) {
-                    const int32_t an = 128 - static_cast<int32_t>(pm[k]);
-                    sumSq += static_cast<int64_t>(an) * an;
-                    const uint32_t lane = (k / 16) * 16 + r, j = k % 16;  // one K step: k < 64
-                    out.tileA[(static_cast<size_t>(tile) * kLanes + lane) * 16 + j] = static_cast<int8_t>(an);
-                }
-                const int64_t q = static_cast<int64_t>(out.constantWeight[x]) + sumSq;
-                out.tileP[static_cast<size_t>(tile) * kTileRows + r] = static_cast<int32_t>(q >> 1);  // floor
-                t.rowEntry[static_cast<size_t>(tile) * kTileRows + r]            = x;
-                t.rowDensityInMixture[static_cast<size_t>(tile) * kTileRows + r] = x - ms.mixture_offsets[shard.begin + mi];
+                place(cls[c][i], tile, 4 * (g0 + slot / 4) + slot % 4);  // rows 4g..4g+3 belong to lane group g
             }
         }
+        for (size_t i = 0; i < rest.size(); ++i)
+            place(rest[i], t0 + pl.nc + static_cast<uint32_t>(i / 16), static_cast<uint32_t>(i % 16));
         t.mixTileOffset[mi + 1] = t.nTiles;
     }
     out.idxBits   = 0;
