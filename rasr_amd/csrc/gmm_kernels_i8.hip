@@ -635,12 +635,14 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             // SCORE_ONLY mixed step: the parity of this lane's row r in each tile (row 4g + r of mixed tile i is
             // remainder entry 16 i + 4g + r, odd from er on; the stand-in's rows never win either way)
             int        pA[4] = {}, pB[4] = {};
-            const auto parities = [&]() {  // p = (row index >= er) as a sign bit: no compare + select
+            // p = (row index >= er) as the sign bit of thr - r: a shift the compiler may not turn into a compare
+            // and a v_cndmask (11.5 cycles per wave64 against 2.9)
+            const auto parities = [&]() {
                 const int thr = static_cast<int>(er) - 16 * static_cast<int>(t - tCls) - 4 * g - 1;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    pA[r] = static_cast<int>(static_cast<uint32_t>(thr - r) >> 31);
-                    pB[r] = static_cast<int>(static_cast<uint32_t>(thr - 16 - r) >> 31);
+                    asm("v_lshrrev_b32 %0, 31, %1" : "=v"(pA[r]) : "v"(thr - r));
+                    asm("v_lshrrev_b32 %0, 31, %1" : "=v"(pB[r]) : "v"(thr - 16 - r));
                 }
             };
             const auto epilogueMixed = [&](int cb) {
