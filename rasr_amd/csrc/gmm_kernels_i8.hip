@@ -593,13 +593,12 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         const int8_t*  base   = lds + (s & 1u) * kSegBytes;
         const uint32_t segT0  = T0 + s * kSegTiles;
         const uint32_t segEnd = min(segT0 + kSegTiles, T1);
-        uint32_t       t      = segT0;
-        while (t < segEnd) {
-            const uint32_t lt = t - segT0;
-            // two tiles of the same mixture (SCORE_ONLY: of the same kind), or the last one beside the
-            // never-winning stand-in: 2 NF independent MFMAs, one v_min3 per candidate pair
-            const bool          mixed = SCORE_ONLY && t >= tCls;  // uniform
-            const bool          two   = t + 1 < segEnd && t + 1 < tEnd && (!SCORE_ONLY || (t + 1 >= tCls) == mixed);
+        // one pair step at tile t: two tiles of the same mixture (SCORE_ONLY: of the same kind), or the last one
+        // beside the never-winning stand-in: 2 NF independent MFMAs, one v_min3 per candidate pair.  kind: 0 key
+        // layout, 1 class tiles, 2 mixed tiles
+        const auto step = [&](const uint32_t t, const bool two, auto kindC) {
+            constexpr int       kKind = decltype(kindC)::value;
+            const uint32_t      lt    = t - segT0;
             const int8_t* const dummy = lds + 2 * kSegBytes;
             const int8_t* const a0    = base + lt * kTileA;
             const int8_t* const a1    = two ? a0 + kTileA : dummy;
@@ -619,7 +618,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             tileRows(p1, c1, P1, T1w);
             i32x4      accA[NF], accB[NF];
             const auto mfmas = [&](int cb) {
-                if constexpr (SCORE_ONLY) {  // the row constants enter as the accumulator input
+                if constexpr (kKind != 0) {  // the row constants enter as the accumulator input
                     accA[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0[0], B[cb][0], P0, 0, 0, 0);
                     accB[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1[0], B[cb][0], P1, 0, 0, 0);
                     return;
@@ -658,7 +657,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             const auto epilogue = [&](int cb) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    if constexpr (SCORE_ONLY) {
+                    if constexpr (kKind == 1) {
                         // a compiler-visible min (not inline asm): the accumulators are read soon after their
                         // MFMAs, and only compiler-visible reads get the hazard wait states.  The empty asm keeps
                         // each update one v_min3 (the compiler would reassociate the chain into v_min pairs)
@@ -707,19 +706,43 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 for (int cb = NF - kLag; cb < NF; ++cb)
                     epi(cb);
             };
-            if constexpr (SCORE_ONLY) {
-                if (mixed) {  // uniform; a few tiles per mixture: the key layout's lag
-                    if (t == tCls)  // the mixture's first mixed tile
-                        toMixed(m);
-                    parities();
-                    pipeline(std::integral_constant<int, 1>{}, epilogueMixed);
-                }
-                else
-                    pipeline(std::integral_constant<int, 3>{}, epilogue);
+            if constexpr (kKind == 2) {  // a few tiles per mixture: the key layout's lag
+                parities();
+                pipeline(std::integral_constant<int, 1>{}, epilogueMixed);
             }
             else
-                pipeline(std::integral_constant<int, 1>{}, epilogue);
-            t += two ? 2u : 1u;
+                pipeline(std::integral_constant<int, kKind == 1 ? 3 : 1>{}, epilogue);
+        };
+        const std::integral_constant<int, 0> kKeyed{};
+        const std::integral_constant<int, 1> kClass{};
+        const std::integral_constant<int, 2> kMixed{};
+        uint32_t t = segT0;
+        while (t < segEnd) {
+            if constexpr (SCORE_ONLY) {
+                // this mixture's class tiles in this segment (a loop with no kind or mixture test per step), then
+                // its mixed ones
+                const uint32_t cEnd = min(segEnd, tCls);
+                while (t < cEnd) {
+                    const bool two = t + 1 < cEnd;
+                    step(t, two, kClass);
+                    t += two ? 2u : 1u;
+                }
+                const uint32_t mEnd = min(segEnd, tEnd);
+                if (t < mEnd) {
+                    if (t == tCls)  // the mixture's first mixed tile: its class minima become 2 v + p_g
+                        toMixed(m);
+                    do {
+                        const bool two = t + 1 < mEnd;
+                        step(t, two, kMixed);
+                        t += two ? 2u : 1u;
+                    } while (t < mEnd);
+                }
+            }
+            else {
+                const bool two = t + 1 < segEnd && t + 1 < tEnd;
+                step(t, two, kKeyed);
+                t += two ? 2u : 1u;
+            }
             // the mixture ending here, and further ones without tiles ending at the same point (rare)
             if (t == tEnd && m < m1) {
                 emit(m, kHot);
