@@ -11,6 +11,6 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -mllvm -amdgpu-mfma-vgpr-form $flags \
       -c rasr_amd/csrc/gmm_kernels_i8.hip -o build/variants/i8_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o rasr_amd/lib/variants/librasr_gmm_$name.so \
-      $OBJS build/variants/i8_$name.o -lz -pthread
+      $OBJS build/variants/i8_$name.o -lz -pthread -lrccl
   echo built $name
 done
