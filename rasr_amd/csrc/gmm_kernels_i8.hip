@@ -568,11 +568,12 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     const std::true_type  kHot{};
     const std::false_type kEmpty{};
     resetBest();
-    const auto mixWord = [&]() {
+    // mixture m starts at tile tBeg (the previous mixture's end: no second load of its offset)
+    const auto mixWord = [&](uint32_t tBeg) {
         if constexpr (SCORE_ONLY) {
             if (m < m1) {
                 const uint32_t w = mixOddMask[m];
-                tCls             = mixTileOff[m] + (w >> 16);
+                tCls             = tBeg + (w >> 16);
                 er               = (w >> 4) & 0xfffu;
             }
         }
@@ -583,7 +584,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         ++m;
         tEnd = m < m1 ? mixTileOff[m + 1] : T1;
     }
-    mixWord();
+    mixWord(T0);
 
     for (uint32_t s = 0; s < nSeg; ++s) {
         // this segment's pieces (issued one segment ago) have landed; the next segment's stay in flight
@@ -757,7 +758,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                     ++m;
                     tEnd = m < m1 ? mixTileOff[m + 1] : T1;
                 }
-                mixWord();
+                mixWord(t);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
