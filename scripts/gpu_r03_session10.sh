@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-3 session 10 (HEAD: score-only paths, class + mixed tiles): GPU tests + smoke, PMC summaries for this
+# build's kernels (fp32, SIMD keyed, batch-int, SIMD scores-only), the default bench line and its rocprofv3
+# kernel-trace summary.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${RUN:-r03_s10}
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>; ALLOW_FAIL=1: a plain failure (rc 1: failed tests) does not stop the run
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -3 $OUT/$name.log
+  if [ $rc -eq 1 ] && [ -n "$ALLOW_FAIL" ]; then return 0; fi
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+ALLOW_FAIL=1 step pytest 1100 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+for mode in fp32 simd bint simd-scores; do
+  step pmc_$mode 600 bash scripts/profile_pmc.sh $mode
+done
+python scripts/pmc_summary.py gpurun_out/pmc_fp32 scoreSplit --json $OUT/pmc_fp32.json > /dev/null || exit 1
+for mode in simd bint simd-scores; do
+  python scripts/pmc_summary.py gpurun_out/pmc_$mode scoreI8 --json $OUT/pmc_$mode.json > /dev/null || exit 1
+done
+cp $OUT/pmc_*.json profiles/
+step bench 900 python bench.py --gpus 1 --steps 20 --warmup 5
+step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off --host-boundary off --extras off
+echo done
