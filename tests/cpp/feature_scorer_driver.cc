@@ -155,6 +155,17 @@ static int benchMain(int argc, char** argv) {
         }
         double   sink  = 0;
         uint64_t sinkB = 0;
+        // search-like consumer: 64 scattered active sets (ascending emission indices), one per frame in turn,
+        // drawn before the timed segment so that the consumer's own cost is the reads alone
+        std::vector<std::vector<uint32_t>> active;
+        if (permille < 1000) {
+            Rng sel{777};
+            active.resize(64);
+            for (auto& a : active)
+                for (uint32_t e = 0; e < M; ++e)
+                    if (sel.next() % 1000u < permille)
+                        a.push_back(e);
+        }
         uint32_t frameNo = 0;
         auto     consume = [&](const Mm::Gpu::Scorer& s) {
             const uint32_t n   = s->nEmissions();
@@ -162,12 +173,9 @@ static int benchMain(int argc, char** argv) {
             if (permille >= 1000)
                 for (uint32_t e = 0; e < n; ++e)
                     acc += s->score(e);
-            else {  // every emission whose (frame, e) hash falls below the share
-                const uint64_t f = 0x9e3779b97f4a7c15ull * ++frameNo;
-                for (uint32_t e = 0; e < n; ++e)
-                    if (((f ^ (e * 0xbf58476d1ce4e5b9ull)) >> 33) % 1000u < permille)
-                        acc += s->score(e);
-            }
+            else
+                for (uint32_t e : active[frameNo++ & 63u])
+                    acc += s->score(e);
             sink += acc;
             if (readBest && s->hasBestDensity())
                 for (uint32_t e = 0; e < n; ++e)
