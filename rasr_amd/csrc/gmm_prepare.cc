@@ -399,8 +399,12 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
     for (uint32_t c = 0; c < C; ++c)
         for (uint32_t k = 0; k < D; ++k)
             out.isvDevice[static_cast<size_t>(c) * out.kSteps * kI8K + k] = out.isvScaled[static_cast<size_t>(c) * D + k];
-    if (scoreOnlyLayout && C == 1 && out.kSteps == 1 && classLayoutFits(ms, shard, out))
-        return buildClassLayout(ms, shard, out);
+    // a mixture whose plan does not fit the mixture word keeps the whole model on the key layout
+    if (scoreOnlyLayout && C == 1 && out.kSteps == 1 && classLayoutFits(ms, shard, out) &&
+        buildClassLayout(ms, shard, out).empty())
+        return "";
+    out.scoreOnly = false;
+    out.mixOddMask.clear();
 
     // device tiles
     buildTiling(ms, shard, out.tiling);
