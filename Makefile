@@ -27,8 +27,9 @@ OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_ke
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 REFSORT   = $(BUILD)/tests/refsort_test
+CLASSLAYOUT = $(BUILD)/tests/class_layout_test
 
-all: $(LIB) $(DRIVER) $(REFSORT) oracle check-integration
+all: $(LIB) $(DRIVER) $(REFSORT) $(CLASSLAYOUT) oracle check-integration
 
 $(BUILD)/gmm_kernels_i8.o: $(SRC)/gmm_kernels_i8.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -120,6 +121,12 @@ $(BUILD)/MixtureSetEstimatorFile.o: $(SRC)/host/MixtureSetEstimatorFile.cc $(HDR
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz -pthread -lrccl
+
+# host check of the score-only layout against the SCORE_ONLY kernel's arithmetic (no GPU)
+$(CLASSLAYOUT): tests/cpp/class_layout_test.cc $(BUILD)/gmm_prepare.o $(HDRS)
+	@mkdir -p $(BUILD)/tests
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@.o
+	$(HIPCC) -o $@ $@.o $(BUILD)/gmm_prepare.o
 
 # host pin of the GPU std::sort replay (gmm_refsort.hh) against this image's std::sort
 $(REFSORT): tests/cpp/refsort_test.cc $(SRC)/gmm_refsort.hh

@@ -77,10 +77,13 @@ struct PreparedQuantized {
     std::vector<int8_t>  tileA;       // [nTiles][kSteps][64 lanes][16]
     std::vector<int32_t> tileP;       // [nTiles][16]
     std::vector<float>   isvDevice;   // [C][kSteps*64], zero padded
-    // score-only class layout (batch types: no best density; one covariance, one K step): a mixture's rows
-    // are split by the parity of Q = c + sum a'^2 over the tile's 4 lane groups (bit g of mixOddMask[m]:
-    // lane group g holds odd-Q rows), and tileP holds the MFMA's C input h = Q >> 1, so the accumulator is
-    // v = dot + h and the row value 2 dot + Q = 2 v + p with p fixed per lane group (gmm_kernels_i8.hip)
+    // score-only class layout (calls without best densities; one covariance, one K step): tileP holds the
+    // MFMA's C input h = Q >> 1 (Q = c + sum a'^2), so the accumulator is v = dot + h and the row value
+    // 2 dot + Q = 2 v + p.  A mixture's class tiles split its rows by the parity p over the tile's 4 lane
+    // groups (bit g of mixOddMask[m]: lane group g holds odd-Q rows); its mixed tiles that follow hold the
+    // rest, evens first in row order (gmm_prepare.cc buildClassLayout, gmm_kernels_i8.hip SCORE_ONLY).
+    // mixOddMask[m]: bits 0-3 the odd lane groups, bits 4-15 the first odd index of the mixed rows, bits
+    // 16-31 the class tile count.
     bool                 scoreOnly = false;
     std::vector<uint32_t> mixOddMask;  // [nMixtures]
 };
