@@ -340,9 +340,6 @@ extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 // (the packed row constant XOR 2^31) and compared unsigned, so OR-ing the sign-extended mask byte of a
 // (frame, density cluster) that the frame did not select makes the all-ones key, which never wins; the
 // segment carries each tile's 16 row offsets into the wave's mask table (gmm_kernels_presel.hip).
-#ifndef GMM_I8_MIXED_LAG
-#define GMM_I8_MIXED_LAG 1  // SCORE_ONLY mixed steps: column blocks between a block's MFMAs and its epilogue
-#endif
 #ifndef GMM_I8_WAVES
 #define GMM_I8_WAVES 4  // scoreI8Seg, one K step: waves per SIMD the register allocation must allow (0 = free)
 #endif
@@ -710,9 +707,9 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 for (int cb = NF - kLag; cb < NF; ++cb)
                     epi(cb);
             };
-            if constexpr (kKind == 2) {
+            if constexpr (kKind == 2) {  // lag 1: 1, 2, 3 measured within noise
                 parities();
-                pipeline(std::integral_constant<int, GMM_I8_MIXED_LAG>{}, epilogueMixed);
+                pipeline(std::integral_constant<int, 1>{}, epilogueMixed);
             }
             else
                 pipeline(std::integral_constant<int, kKind == 1 ? 3 : 1>{}, epilogue);

@@ -186,10 +186,7 @@ static ShardRange normalizeShard(const gmm_mixture_set& ms, ShardRange s) {
 // tiles, bits 4-15 er, bits 16-31 nc.
 static constexpr int32_t kClassPadC  = 0x30000000;
 static constexpr int64_t kClassLimit = int64_t(1) << 29;  // |2 dot + Q| bound of a real row
-#ifndef GMM_CLASS_MIXED_COST
-#define GMM_CLASS_MIXED_COST 1.25
-#endif
-static constexpr double  kMixedCost  = GMM_CLASS_MIXED_COST;  // a mixed pair step against a class pair step
+static constexpr double  kMixedCost  = 1.25;               // a mixed pair step against a class pair step
 
 // false: some row's |2 dot + Q| may reach kClassLimit; the key layout is used instead
 static bool classLayoutFits(const gmm_mixture_set& ms, ShardRange shard, const PreparedQuantized& out) {
