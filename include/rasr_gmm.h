@@ -173,9 +173,19 @@ int gmm_score_host(gmm_scorer* scorer, const float* frames, uint32_t n_frames, u
  *   asked (AssigningFeatureScorer.hh:110-121): a search that reads only score(e) never pays for the
  *   assignment. */
 #define GMM_HOST_LAZY_BEST 4u
+/* flags: GMM_HOST_ASYNC: the call returns once its copies and kernels are enqueued; its tables are written when
+ *   gmm_host_call_wait(scorer, call_id) returns (or any later host call of the scorer, which waits for it
+ *   first).  The score (and best) tables must be page-locked (gmm_host_alloc); the ring rows of the call are read
+ *   asynchronously and must not change until the wait.  The drop-in's ring buffer uses it to score the newest
+ *   frames on the GPU while the caller consumes the older ones. */
+#define GMM_HOST_ASYNC 8u
 int gmm_score_host_ring(gmm_scorer* scorer, const float* ring, uint32_t ring_size, uint32_t first,
                         uint32_t n_frames, uint32_t frame_stride, float* scores, uint32_t* best_density,
                         uint32_t score_stride, uint32_t flags, uint64_t* call_id);
+
+/* Waits for host call `call_id` (made with GMM_HOST_ASYNC; any other call id returns at once).  Status of the
+ * call's device work. */
+int gmm_host_call_wait(gmm_scorer* scorer, uint64_t call_id);
 
 /* Best densities of host call `call_id` (made with GMM_HOST_KEEP_BEST or GMM_HOST_LAZY_BEST) into the same ring positions of
  * best_density, in the same layout, that its scores went to.  GMM_ERR_INVALID_ARGUMENT once a later

@@ -92,6 +92,7 @@ class EstimatorConfig(ctypes.Structure):
 GMM_HOST_KEEP_BEST = 1
 GMM_HOST_FRAME_MAJOR = 2
 GMM_HOST_LAZY_BEST = 4
+GMM_HOST_ASYNC = 8
 # gmm_scorer_create_sharded: the per-frame reduce of mixtures split between GPUs
 GMM_EXCHANGE = {"auto": 0, "rccl": 1, "copy": 2}
 
@@ -115,6 +116,7 @@ PROTOTYPES = [
     ("gmm_score_host_ring", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
+    ("gmm_host_call_wait", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     ("gmm_fetch_best_density", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]),
     ("gmm_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     ("gmm_host_free", ctypes.c_int, [ctypes.c_void_p]),

@@ -158,6 +158,9 @@ struct gmm_scorer {
     // host calls (gmm_score_host*): id of the last one; the one whose best densities dHostBest keeps
     // (GMM_HOST_KEEP_BEST) with its ring mapping and copy segments, for gmm_fetch_best_density
     uint64_t                 hostCall = 0, keptBestCall = 0;
+    // GMM_HOST_ASYNC: the host call in flight (0: none) and its completion, recorded on hostCopy
+    uint64_t                 asyncCall = 0;
+    hipEvent_t               asyncDone = nullptr;
     HostRing                 keptRing{};
     std::vector<HostSegment> keptSegs;
     bool                     keptFrameMajor = false;
@@ -193,7 +196,9 @@ struct gmm_scorer {
         }
         for (hipEvent_t ev : chunkDone)
             (void)hipEventDestroy(ev);
-        for (hipEvent_t ev : {hostStart, stageDone[0], stageDone[1]})
+        if (asyncCall && asyncDone)
+            (void)hipEventSynchronize(asyncDone);  // no DMA into a caller's table may outlive the scorer
+        for (hipEvent_t ev : {hostStart, stageDone[0], stageDone[1], asyncDone})
             if (ev)
                 (void)hipEventDestroy(ev);
         for (hipStream_t st : {hostCompute, hostCopy})
@@ -302,6 +307,18 @@ struct TimedSpan {
 
 int groupScore(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
                uint32_t* best, uint32_t scoreStride, hipStream_t stream);
+
+// the GMM_HOST_ASYNC call in flight, if any, is complete on return: its staging (frames, prepared frames,
+// device tables) is free for the next call of any kind
+int waitAsync(gmm_scorer* s) {
+    if (!s->asyncCall)
+        return GMM_OK;
+    s->asyncCall       = 0;
+    const hipError_t e = hipEventSynchronize(s->asyncDone);
+    if (e != hipSuccess)
+        return fail(GMM_ERR_DEVICE, std::string("hipEventSynchronize (GMM_HOST_ASYNC call): ") + hipGetErrorString(e));
+    return GMM_OK;
+}
 
 int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, float* scores,
               uint32_t* best, uint32_t scoreStride, hipStream_t stream) {
@@ -596,7 +613,7 @@ void appendSegments(const HostRing& r, uint32_t k, uint32_t t0, uint32_t n, std:
 // columns of [nMix][scoreStride]; frame-major: their transposes [nFrames][nMix] (dHostScoresT, dHostBestT)
 // into rows of [ringSize][scoreStride].
 int copyOutTables(gmm_scorer* s, const std::vector<HostSegment>& segs, uint32_t nFrames, bool frameMajor, float* scores,
-                  uint32_t* best, uint32_t scoreStride) {
+                  uint32_t* best, uint32_t scoreStride, bool async = false) {
     struct Table {
         char*       dst;
         const char* src;
@@ -673,6 +690,8 @@ int copyOutTables(gmm_scorer* s, const std::vector<HostSegment>& segs, uint32_t 
             });
         }
     }
+    if (async)  // page-locked destinations only (checked by the caller): nothing was staged
+        return GMM_OK;
     GMM_HIP_CHECK(hipStreamSynchronize(s->hostCopy));
     return GMM_OK;
 }
@@ -691,7 +710,7 @@ int transposeChunk(gmm_scorer* s, bool scores, bool best, uint32_t t0, uint32_t 
 }
 
 int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, uint32_t scoreStride, bool keepBest,
-                  bool lazyBest, bool frameMajor) {
+                  bool lazyBest, bool frameMajor, bool async) {
     const uint32_t fpb = framesPerBlock(s), nFrames = r.nFrames;
     // frame chunks for large tables; one chunk for preselection (gmm_scorer_cluster_selection reports the
     // last call's whole batch)
@@ -726,9 +745,16 @@ int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* bes
             return rc;
         GMM_HIP_CHECK(hipEventRecord(s->chunkDone[k], s->hostCompute));
     }
-    if ((rc = copyOutTables(s, segs, nFrames, frameMajor, scores, best, scoreStride)) != GMM_OK)
+    if ((rc = copyOutTables(s, segs, nFrames, frameMajor, scores, best, scoreStride, async)) != GMM_OK)
         return rc;
-    GMM_HIP_CHECK(hipStreamSynchronize(s->hostCompute));
+    if (async) {  // the copies wait for every chunk: their end is the call's end
+        if (!s->asyncDone)
+            GMM_HIP_CHECK(hipEventCreateWithFlags(&s->asyncDone, hipEventDisableTiming));
+        GMM_HIP_CHECK(hipEventRecord(s->asyncDone, s->hostCopy));
+        s->asyncCall = s->hostCall;
+    }
+    else
+        GMM_HIP_CHECK(hipStreamSynchronize(s->hostCompute));
     if (keepBest) {
         s->keptBestCall  = s->hostCall;
         s->keptRing      = r;
@@ -752,8 +778,14 @@ int scoreHost(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, u
               uint64_t* callId) {
     if (!s)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
-    if ((flags & ~(GMM_HOST_KEEP_BEST | GMM_HOST_FRAME_MAJOR | GMM_HOST_LAZY_BEST)) != 0)
+    if ((flags & ~(GMM_HOST_KEEP_BEST | GMM_HOST_FRAME_MAJOR | GMM_HOST_LAZY_BEST | GMM_HOST_ASYNC)) != 0)
         return fail(GMM_ERR_INVALID_ARGUMENT, "unknown flags");
+    const bool async = (flags & GMM_HOST_ASYNC) != 0;
+    if (async && ((scores && !isPinnedHost(scores)) || (best && !isPinnedHost(best))))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_ASYNC needs page-locked score / best tables (gmm_host_alloc)");
+    int wrc = waitAsync(s);  // the previous asynchronous call's staging and tables
+    if (wrc != GMM_OK)
+        return wrc;
     const bool frameMajor = (flags & GMM_HOST_FRAME_MAJOR) != 0;
     if ((flags & GMM_HOST_KEEP_BEST) && (flags & GMM_HOST_LAZY_BEST))
         return fail(GMM_ERR_INVALID_ARGUMENT, "GMM_HOST_KEEP_BEST and GMM_HOST_LAZY_BEST together");
@@ -785,7 +817,7 @@ int scoreHost(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, u
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostScoresT), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(float)));
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostBestT), maxF * std::max<uint32_t>(s->nMix, 1) * sizeof(uint32_t)));
     }
-    const int rc = scoreHostImpl(s, r, scores, best, scoreStride, keepBest, lazyBest, frameMajor);
+    const int rc = scoreHostImpl(s, r, scores, best, scoreStride, keepBest, lazyBest, frameMajor, async);
     if (rc != GMM_OK)
         for (hipStream_t st : {s->hostCompute, s->hostCopy})
             if (st)
@@ -1393,6 +1425,9 @@ int gmm_score_device(gmm_scorer* s, const float* frames, uint32_t nFrames, uint3
                      uint32_t* best, uint32_t scoreStride, void* stream) {
     if (!s)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    const int wrc = waitAsync(s);  // a GMM_HOST_ASYNC call still uses the frame staging
+    if (wrc != GMM_OK)
+        return wrc;
     return scoreImpl(s, frames, nFrames, frameStride, scores, best, scoreStride, static_cast<hipStream_t>(stream));
 }
 
@@ -1408,9 +1443,18 @@ int gmm_score_host_ring(gmm_scorer* s, const float* ring, uint32_t ringSize, uin
     return scoreHost(s, HostRing{ring, ringSize, first, nFrames, frameStride}, scores, best, scoreStride, flags, callId);
 }
 
+int gmm_host_call_wait(gmm_scorer* s, uint64_t callId) {
+    if (!s)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+    return callId != 0 && callId == s->asyncCall ? waitAsync(s) : GMM_OK;
+}
+
 int gmm_fetch_best_density(gmm_scorer* s, uint64_t callId, uint32_t* best, uint32_t scoreStride) {
     if (!s || !best)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    const int wrc = waitAsync(s);
+    if (wrc != GMM_OK)
+        return wrc;
     if (!hasAssignment(s))
         return fail(GMM_ERR_UNSUPPORTED, "scorer type has no best densities (batch types)");
     if (callId == 0 || callId != s->keptBestCall)

@@ -329,19 +329,78 @@ std::unique_ptr<GpuBatchFeatureScorer> GpuBatchFeatureScorer::create(const Mixtu
     s->cached_.assign(b, 0);
     s->bestCached_.assign(b, 0);
     s->bestCall_.assign(b, 0);
+    s->inflight_.assign(b, 0);
+    s->prefetchChunk_ = b >= kPrefetchMin ? b / 4 : 0;
     return s;
+}
+
+GpuBatchFeatureScorer::~GpuBatchFeatureScorer() {
+    if (asyncCall_)  // no DMA into the tables after they are freed
+        (void)gmm_host_call_wait(handle_, asyncCall_);
 }
 
 // BatchFeatureScorerBase::reset, BatchFeatureScorer.cc:40-44
 void GpuBatchFeatureScorer::reset() const {
+    if (asyncCall_)
+        (void)gmm_host_call_wait(handle_, asyncCall_);
+    asyncCall_ = 0;
+    std::fill(inflight_.begin(), inflight_.end(), 0);
     std::fill(cached_.begin(), cached_.end(), 0);
+    pendingCount_   = 0;
     currentFeature_ = 0;
     buffered_       = 0;
 }
 
 void GpuBatchFeatureScorer::setFeature(size_t pos, const FeatureVector& f) const {
     assert(pos < bufferSize_ && f.size() == dimension_);
+    if (inflight_[pos])  // its row may not have been read yet (a context whose scores were never asked for)
+        landInflight();
     std::copy(f.begin(), f.end(), features_.data() + pos * dimension_);
+    if (!prefetchChunk_ || bestWanted_)
+        return;
+    // the new frame joins the pending run (it is the newest buffered position)
+    if (pendingCount_ == 0)
+        pendingFirst_ = static_cast<uint32_t>(pos);
+    if ((pendingFirst_ + pendingCount_) % bufferSize_ != pos || pendingCount_ >= bufferSize_) {
+        pendingCount_ = 0;  // not contiguous with the run (cannot happen in the protocol's order): start over
+        pendingFirst_ = static_cast<uint32_t>(pos);
+    }
+    ++pendingCount_;
+    if (pendingCount_ >= prefetchChunk_)
+        submitPending();
+}
+
+void GpuBatchFeatureScorer::landInflight() const {
+    if (!asyncCall_)
+        return;
+    if (gmm_host_call_wait(handle_, asyncCall_) != GMM_OK)
+        criticalError("gmm_host_call_wait");
+    for (uint32_t q = 0; q < bufferSize_; ++q)
+        if (inflight_[q]) {
+            inflight_[q]   = 0;
+            cached_[q]     = 1;
+            bestCached_[q] = 0;
+            bestCall_[q]   = asyncCall_;
+        }
+    asyncCall_ = 0;
+}
+
+void GpuBatchFeatureScorer::submitPending() const {
+    landInflight();  // one call in flight at a time (the library's staging)
+    uint64_t call = 0;
+    ++launches_;
+    if (gmm_score_host_ring(handle_, features_.data(), bufferSize_, pendingFirst_, pendingCount_, dimension_, scores_.data(),
+                            nullptr, rowStride(),
+                            GMM_HOST_FRAME_MAJOR | GMM_HOST_ASYNC | (assigning_ ? GMM_HOST_LAZY_BEST : 0u), &call) != GMM_OK)
+        criticalError("gmm_score_host_ring");
+    for (uint32_t i = 0; i < pendingCount_; ++i) {
+        const uint32_t q = (pendingFirst_ + i) % bufferSize_;
+        inflight_[q]     = 1;
+        cached_[q]       = 0;
+    }
+    asyncCall_    = call;
+    pendingFirst_ = (pendingFirst_ + pendingCount_) % bufferSize_;
+    pendingCount_ = 0;
 }
 
 // BatchFeatureScorerBase::addFeature, BatchFeatureScorer.cc:46-50
@@ -384,6 +443,8 @@ void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
     length           = std::min(length, b);
     const uint32_t p = featureIndex % b;
     uint64_t       call = 0;
+    landInflight();
+    pendingCount_ = 0;  // this fill covers every buffered position from p on
     ++launches_;
     if (gmm_score_host_ring(handle_, features_.data(), b, p, length, dimension_, scores_.data(), nullptr, rowStride(),
                             GMM_HOST_FRAME_MAJOR | (assigning_ ? GMM_HOST_LAZY_BEST : 0u), &call) != GMM_OK)
@@ -400,6 +461,8 @@ void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
 Score GpuBatchFeatureScorer::getScore(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {
     assert(e < nMixtures_);
     const uint32_t p = featureIndex % bufferSize_;
+    if (!cached_[p] && inflight_[p])
+        landInflight();
     if (!cached_[p])
         fill(featureIndex, length);
     return scores_[static_cast<size_t>(p) * rowStride() + e];
@@ -409,7 +472,10 @@ DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t
     assert(e < nMixtures_);
     if (!assigning_)
         return 0xffffffffu;
+    bestWanted_      = true;  // an aligner: no more prefetch (its calls' best densities would not stay kept)
     const uint32_t p = featureIndex % bufferSize_;
+    if (!cached_[p] && inflight_[p])
+        landInflight();
     if (!cached_[p])
         fill(featureIndex, length);
     if (!bestCached_[p]) {

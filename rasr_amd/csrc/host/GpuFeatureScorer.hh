@@ -204,6 +204,7 @@ class GpuBatchFeatureScorer : public FeatureScorer {
 public:
     static std::unique_ptr<GpuBatchFeatureScorer> create(const MixtureSet& ms, const Configuration& c,
                                                           std::string* error = nullptr);
+    ~GpuBatchFeatureScorer() override;
     Scorer   getScorer(const FeatureVector& f) const override;
     void     reset() const override;
     bool     isBuffered() const override { return true; }
@@ -225,6 +226,8 @@ private:
     GpuBatchFeatureScorer() {}
     void     setFeature(size_t pos, const FeatureVector& f) const;
     void     fill(uint32_t featureIndex, uint32_t length) const;
+    void     submitPending() const;   // the pending run as a GMM_HOST_ASYNC call
+    void     landInflight() const;    // wait for the asynchronous call; its positions become cached
     uint32_t rowStride() const { return nMixtures_ ? nMixtures_ : 1; }
 
     uint32_t bufferSize_ = 4;
@@ -243,6 +246,17 @@ private:
     mutable std::vector<char> cached_;       // [bufferSize] scores of the position are in scores_
     mutable std::vector<char> bestCached_;   // [bufferSize] best densities of the position are in best_
     mutable std::vector<uint64_t> bestCall_; // [bufferSize] host call that scored the position
+    // Prefetch (buffers of kPrefetchMin frames and more): the newest frames not yet scored (pending: the ring run
+    // [pendingFirst_, pendingFirst_ + pendingCount_)) go to the GPU as one GMM_HOST_ASYNC call once they number
+    // prefetchChunk_, so the GPU scores them while the caller still consumes older positions; a position whose
+    // score is asked for while its call is in flight waits for it (inflight_).  Off once bestDensity() was asked
+    // for (the aligners' best densities are fetched from the newest call only).
+    static constexpr uint32_t kPrefetchMin = 32;
+    uint32_t                  prefetchChunk_ = 0;  // 0: no prefetch
+    mutable std::vector<char> inflight_;           // [bufferSize] scored by asyncCall_, not landed yet
+    mutable uint64_t          asyncCall_    = 0;
+    mutable uint32_t          pendingFirst_ = 0, pendingCount_ = 0;
+    mutable bool              bestWanted_   = false;
     mutable int32_t           currentFeature_ = 0;
     mutable int32_t           buffered_       = 0;
     mutable uint32_t          launches_       = 0, bestFetches_ = 0;

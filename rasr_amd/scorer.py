@@ -171,12 +171,13 @@ class Scorer:
 
     def score_host_ring(self, ring: np.ndarray, first: int, n_frames: int, out: np.ndarray,
                         best_out: np.ndarray | None = None, keep_best: bool = False, frame_major: bool = False,
-                        lazy_best: bool = False) -> int:
+                        lazy_best: bool = False, asynchronous: bool = False) -> int:
         """gmm_score_host_ring: frames ring[(first + i) % R], i < n_frames (R = ring.shape[0]) into the ring
         positions of out / best_out: columns of [n_mixtures][>= R] tables, or with frame_major rows of
         [>= R][>= n_mixtures] tables.  keep_best: best densities stay on the device for fetch_best();
         lazy_best: scores only, fetch_best() computes the best densities from the frames kept on the device.
-        Returns the call id."""
+        asynchronous (GMM_HOST_ASYNC, page-locked tables only): returns once enqueued; wait(call id) before
+        reading the tables or changing the ring rows.  Returns the call id."""
         ring = np.ascontiguousarray(ring, dtype=np.float32)
         m, R = self.n_mixtures(), ring.shape[0]
         for name, a, dt in (("out", out, np.float32), ("best_out", best_out, np.uint32)):
@@ -190,13 +191,17 @@ class Scorer:
             raise ValueError("out and best_out must have the same row stride")
         cid = ctypes.c_uint64()
         flags = ((_capi.GMM_HOST_KEEP_BEST if keep_best else 0) | (_capi.GMM_HOST_FRAME_MAJOR if frame_major else 0) |
-                 (_capi.GMM_HOST_LAZY_BEST if lazy_best else 0))
+                 (_capi.GMM_HOST_LAZY_BEST if lazy_best else 0) | (_capi.GMM_HOST_ASYNC if asynchronous else 0))
         rc = self._lib.gmm_score_host_ring(
             self._h, ring.ctypes.data_as(ctypes.c_void_p), R, int(first), int(n_frames), ring.shape[1],
             out.ctypes.data_as(ctypes.c_void_p), best_out.ctypes.data_as(ctypes.c_void_p) if best_out is not None else None,
             out.shape[1], flags, ctypes.byref(cid))
         _capi.check(rc, "gmm_score_host_ring")
         return cid.value
+
+    def wait(self, call_id: int) -> None:
+        """gmm_host_call_wait: the GMM_HOST_ASYNC call `call_id` has written its tables."""
+        _capi.check(self._lib.gmm_host_call_wait(self._h, int(call_id)), "gmm_host_call_wait")
 
     def fetch_best(self, call_id: int, best_out: np.ndarray) -> None:
         """gmm_fetch_best_density into the same ring columns the call's scores went to."""

@@ -219,12 +219,14 @@ int main(int argc, char** argv) {
     if (argc >= 2 && std::string(argv[1]) == "bench")
         return benchMain(argc, argv);
     if (argc != 7 && argc != 8) {
-        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node]\n", argv[0]);
+        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node|delayed|search]\n",
+                argv[0]);
         return 2;
     }
     const std::string protocol = argc == 8 ? argv[7] : "recognizer";
-    if (protocol != "recognizer" && protocol != "node" && protocol != "delayed")
+    if (protocol != "recognizer" && protocol != "node" && protocol != "delayed" && protocol != "search")
         return 2;
+    const bool search = protocol == "search";  // the recognizer's sequence, score(e) only (no bestDensity)
     const bool     delayed = protocol == "delayed";
     const uint32_t kDelay  = 3;
     std::deque<Mm::Gpu::Scorer> pending;
@@ -282,7 +284,7 @@ int main(int argc, char** argv) {
         const uint32_t n = node ? s->nEmissions() : M;  // the node dumps nEmissions() values per frame
         for (uint32_t e = 0; e < n; ++e) {
             outS.push_back(node ? -s->score(e) : s->score(e));  // FeatureScorerNode::putData: +log space
-            outB.push_back(s->hasBestDensity() ? s->bestDensity(e) : 0xffffffffu);
+            outB.push_back(!search && s->hasBestDensity() ? s->bestDensity(e) : 0xffffffffu);
         }
     };
     const uint32_t segments = static_cast<uint32_t>(atoi(argv[6]));

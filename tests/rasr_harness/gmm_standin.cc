@@ -195,6 +195,12 @@ int gmm_score_host_ring(gmm_scorer* s, const float* ring, uint32_t R, uint32_t f
     return GMM_OK;
 }
 
+// GMM_HOST_ASYNC: the stand-in scores synchronously, so the wait has nothing to wait for
+int gmm_host_call_wait(gmm_scorer* s, uint64_t callId) {
+    (void)callId;
+    return s ? GMM_OK : fail(GMM_ERR_INVALID_ARGUMENT, "null scorer");
+}
+
 int gmm_score_host(gmm_scorer* s, const float* frames, uint32_t n, uint32_t fstride, float* scores, uint32_t* best,
                    uint32_t stride) {
     return gmm_score_host_ring(s, frames, n ? n : 1, 0, n, fstride, scores, best, stride, 0, nullptr);

@@ -188,3 +188,41 @@ def test_fetch_best_after_later_call_is_refused(gpu, model):
     cid = sb.score_host_ring(ring, 3, 16, out, keep_best=True)
     with pytest.raises(ra.GmmError):
         sb.fetch_best(cid, best)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum", "batch-diagonal-maximum-int"])
+def test_async_host_call(gpu, model, kind):
+    """GMM_HOST_ASYNC: the call returns once enqueued; after gmm_host_call_wait the pinned tables hold what a
+    synchronous call writes.  A later call waits for it by itself; pageable tables are refused."""
+    R, first, n = 600, 450, 500  # wraps, several pipeline chunks
+    ring = ra.synthetic_frames(R, 33, seed=71)
+    sc = ra.Scorer(model, kind, max_frames=n)
+    m = sc.n_mixtures()
+    sync = np.zeros((R, m), np.float32)
+    sc.score_host_ring(ring, first, n, sync, frame_major=True, lazy_best=True)
+    out = ra.pinned_empty((R, m), np.float32)
+    out[:] = -1.0
+    cid = sc.score_host_ring(ring, first, n, out, frame_major=True, lazy_best=True, asynchronous=True)
+    sc.wait(cid)
+    pos = (first + np.arange(n)) % R
+    assert np.array_equal(out[pos].view(np.uint32), sync[pos].view(np.uint32))
+    rest = np.ones(R, bool)
+    rest[pos] = False
+    assert (out[rest] == -1.0).all()
+    if kind != "batch-diagonal-maximum-int":  # best densities of the asynchronous call, computed on demand
+        best = ra.pinned_empty((R, m), np.uint32)
+        sc.fetch_best(cid, best)
+        eager = np.zeros((R, m), np.uint32)
+        sc.score_host_ring(ring, first, n, np.zeros((R, m), np.float32), eager, frame_major=True)
+        assert np.array_equal(best[pos], eager[pos])
+    # two asynchronous calls back to back, the second waits for the first; a synchronous one after both
+    out2 = ra.pinned_empty((R, m), np.float32)
+    c1 = sc.score_host_ring(ring, 0, 100, out, frame_major=True, asynchronous=True)
+    c2 = sc.score_host_ring(ring, 100, 100, out2, frame_major=True, asynchronous=True)
+    sc.wait(c1)
+    sc.wait(c2)
+    assert np.array_equal(out2[100:200].view(np.uint32), sync[100:200].view(np.uint32))
+    assert np.array_equal(out[0:100].view(np.uint32), sync[0:100].view(np.uint32))
+    with pytest.raises(ra.GmmError):
+        sc.score_host_ring(ring, 0, 10, np.zeros((R, m), np.float32), frame_major=True, asynchronous=True)

@@ -206,3 +206,47 @@ def test_delayed_consumer_unbuffered(gpu, tmp_path, kind):
         ref_s, ref_b = oracle.OracleFloat(ms).score(frames)[:2]
         assert (np.abs(s.T.astype(np.float64) - ref_s) / np.maximum(1, np.abs(ref_s))).max() <= 1e-4
     assert launches == 2 * 29
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,buffer_size", [("SIMD-diagonal-maximum", 64), ("SIMD-diagonal-maximum", 100),
+                                              ("batch-diagonal-maximum-int", 64), ("diagonal-maximum", 64),
+                                              ("batch-diagonal-maximum-float", 48)])
+def test_prefetch_search_protocol(gpu, tmp_path, kind, buffer_size):
+    """Buffers of 32 frames and more prefetch: the newest quarter of the ring goes to the GPU as a GMM_HOST_ASYNC
+    call (score-only kernels, GMM_HOST_LAZY_BEST) while older positions are consumed.  The recognizer's sequence
+    reading score(e) only, over three segments (reset between them): the same scores as the oracle, fewer launches
+    than frames."""
+    ms = ra.synthetic_mixture_set(40, ra.ragged_counts(40, 40 * 12, low=1, high=30, seed=61), 39, seed=61,
+                                  weights="random")
+    frames = ra.synthetic_frames(701, 39, seed=62)
+    s, b, launches = _run(tmp_path, ms, frames, kind, buffer_size, 3, protocol="search")
+    assert (b == 0xFFFFFFFF).all()
+    if kind == "SIMD-diagonal-maximum":
+        ref = oracle.OracleSimd(ms).score(frames)[0]
+    elif kind == "batch-diagonal-maximum-int":
+        ref = oracle.batch_int_score(ms, frames)
+    elif kind == "diagonal-maximum":
+        ref = oracle.OracleFloat(ms).score(frames)[0]
+    else:
+        ref = oracle.batch_float_score(ms, frames)
+    if kind in ("SIMD-diagonal-maximum", "batch-diagonal-maximum-int"):
+        assert np.array_equal(s.T.view(np.uint32), ref.view(np.uint32))
+    else:
+        err = np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))
+        assert err.max() <= 1e-4
+    assert launches < 701 // 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", ["recognizer", "node"])
+def test_prefetch_then_best_densities(gpu, tmp_path, protocol):
+    """A buffer that prefetches, read by a consumer that asks bestDensity(e) too (the aligners; the node's dump):
+    prefetch stops at the first bestDensity(), the scores and best densities stay bit-exact."""
+    ms = ra.synthetic_mixture_set(30, 9, 39, seed=63, weights="random")
+    frames = ra.synthetic_frames(260, 39, seed=64)
+    s, b, _ = _run(tmp_path, ms, frames, "SIMD-diagonal-maximum", 64, 2, protocol=protocol)
+    ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+    sign = -1.0 if protocol == "node" else 1.0
+    assert np.array_equal((sign * s.T).astype(np.float32).view(np.uint32), ref_s.view(np.uint32))
+    assert np.array_equal(b.T, ref_b)
