@@ -330,7 +330,7 @@ std::unique_ptr<GpuBatchFeatureScorer> GpuBatchFeatureScorer::create(const Mixtu
     s->bestCached_.assign(b, 0);
     s->bestCall_.assign(b, 0);
     s->inflight_.assign(b, 0);
-    s->prefetchChunk_ = b >= kPrefetchMin ? b / 4 : 0;
+    s->prefetchChunk_ = b >= kPrefetchMin ? b / 2 : 0;
     return s;
 }
 

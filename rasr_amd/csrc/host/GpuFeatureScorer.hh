@@ -248,10 +248,10 @@ private:
     mutable std::vector<uint64_t> bestCall_; // [bufferSize] host call that scored the position
     // Prefetch (buffers of kPrefetchMin frames and more): the newest frames not yet scored (pending: the ring run
     // [pendingFirst_, pendingFirst_ + pendingCount_)) go to the GPU as one GMM_HOST_ASYNC call once they number
-    // prefetchChunk_, so the GPU scores them while the caller still consumes older positions; a position whose
+    // prefetchChunk_ (half the ring), so the GPU scores them while the caller still consumes older positions; a position whose
     // score is asked for while its call is in flight waits for it (inflight_).  Off once bestDensity() was asked
     // for (the aligners' best densities are fetched from the newest call only).
-    static constexpr uint32_t kPrefetchMin = 32;
+    static constexpr uint32_t kPrefetchMin = 64;
     uint32_t                  prefetchChunk_ = 0;  // 0: no prefetch
     mutable std::vector<char> inflight_;           // [bufferSize] scored by asyncCall_, not landed yet
     mutable uint64_t          asyncCall_    = 0;

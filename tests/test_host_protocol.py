@@ -211,9 +211,9 @@ def test_delayed_consumer_unbuffered(gpu, tmp_path, kind):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,buffer_size", [("SIMD-diagonal-maximum", 64), ("SIMD-diagonal-maximum", 100),
                                               ("batch-diagonal-maximum-int", 64), ("diagonal-maximum", 64),
-                                              ("batch-diagonal-maximum-float", 48)])
+                                              ("batch-diagonal-maximum-float", 80)])
 def test_prefetch_search_protocol(gpu, tmp_path, kind, buffer_size):
-    """Buffers of 32 frames and more prefetch: the newest quarter of the ring goes to the GPU as a GMM_HOST_ASYNC
+    """Buffers of 64 frames and more prefetch: the newest half of the ring goes to the GPU as a GMM_HOST_ASYNC
     call (score-only kernels, GMM_HOST_LAZY_BEST) while older positions are consumed.  The recognizer's sequence
     reading score(e) only, over three segments (reset between them): the same scores as the oracle, fewer launches
     than frames."""
