@@ -219,7 +219,13 @@ public:
     BufferedScorer(const GpuBatchFeatureScorer* parent, uint32_t currentFeature, uint32_t buffered, bool assigning)
             : parent_(parent), currentFeature_(currentFeature), buffered_(buffered), assigning_(assigning) {}
     EmissionIndex nEmissions() const override { return parent_->nMixtures(); }
-    Score         score(EmissionIndex e) const override { return parent_->getScore(e, currentFeature_, buffered_); }
+    // the first score(e) fills the position if needed and keeps its row of the frame-major table: the row stays
+    // valid while the context is (the protocol reuses the position only at a later getScorer())
+    Score score(EmissionIndex e) const override {
+        if (!row_)
+            row_ = parent_->scoreRow(currentFeature_, buffered_);
+        return row_[e];
+    }
     bool             hasBestDensity() const override { return assigning_; }
     DensityInMixture bestDensity(EmissionIndex e) const override {
         return parent_->getBestDensity(e, currentFeature_, buffered_);
@@ -229,6 +235,7 @@ private:
     const GpuBatchFeatureScorer* parent_;
     uint32_t                     currentFeature_, buffered_;
     bool                         assigning_;
+    mutable const float*         row_ = nullptr;
 };
 
 }  // namespace
@@ -460,12 +467,16 @@ void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
 // BatchFeatureScorerBase::getScore, BatchFeatureScorer.cc:98-105
 Score GpuBatchFeatureScorer::getScore(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {
     assert(e < nMixtures_);
+    return scoreRow(featureIndex, length)[e];
+}
+
+const float* GpuBatchFeatureScorer::scoreRow(uint32_t featureIndex, uint32_t length) const {
     const uint32_t p = featureIndex % bufferSize_;
     if (!cached_[p] && inflight_[p])
         landInflight();
     if (!cached_[p])
         fill(featureIndex, length);
-    return scores_[static_cast<size_t>(p) * rowStride() + e];
+    return scores_.data() + static_cast<size_t>(p) * rowStride();
 }
 
 DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {

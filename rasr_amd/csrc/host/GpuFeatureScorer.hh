@@ -215,6 +215,9 @@ public:
     uint32_t bufferSize() const override { return bufferSize_; }
 
     Score            getScore(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
+    // the scores of every emission of the buffered position featureIndex (filled first if needed): nMixtures()
+    // floats of the page-locked frame-major table, valid until the protocol reuses the position
+    const float*     scoreRow(uint32_t featureIndex, uint32_t length) const;
     // 0xffffffff for the batch types, which have no assignment (as ContextScorer::bestDensity)
     DensityInMixture getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
 
