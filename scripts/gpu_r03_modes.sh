@@ -18,6 +18,8 @@ step() {
 step sharded_tests 400 python -u -m pytest tests/test_sharded_scorer.py -q -m gpu --timeout 120 --timeout-method thread
 B="--gpus 1 --steps 20 --warmup 3 --cpu-baseline off --host-boundary off --extras off --no-extra-mode"
 step bench_sum 300 python bench.py --mode sum $B
+step bench_sum_scores 300 python bench.py --mode sum --no-best $B
+step bench_d45_simd_scores 300 python bench.py --dim 45 --mode simd-scores $B
 step bench_presel_int 300 python bench.py --mode presel-int $B
 step bench_presel_float 300 python bench.py --mode presel-float $B
 step bench_nn 300 python bench.py --mode nn $B
