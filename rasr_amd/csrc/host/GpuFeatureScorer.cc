@@ -497,10 +497,20 @@ DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t
                 if (cached_[q] && bestCall_[q] == call)
                     bestCached_[q] = 1;
         }
+        else if (fill(featureIndex, length),
+                 gmm_fetch_best_density(handle_, bestCall_[p], best_.data(), rowStride()) == GMM_OK) {
+            // a later call replaced its frames on the device (e.g. a prefetch before the first bestDensity()):
+            // the buffered positions from p scored again in one call (the same score-only values), their best
+            // densities computed from it
+            ++bestFetches_;
+            const uint64_t refill = bestCall_[p];
+            for (uint32_t q = 0; q < bufferSize_; ++q)
+                if (cached_[q] && bestCall_[q] == refill)
+                    bestCached_[q] = 1;
+        }
         else {
-            // a later fill replaced its frames on the device: score this position again (its row of features_
-            // is unchanged while cached_[p] holds), best densities copied directly into its row of best_, the
-            // scores into scratch (the row of scores_ keeps the score-only values it already returned)
+            // (not reached with this library: the fill above is the newest call) score this position again,
+            // best densities copied directly into its row of best_, the scores into scratch
             uint64_t again = 0;
             ++launches_;
             scratch_.resize(rowStride());

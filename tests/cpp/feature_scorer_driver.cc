@@ -219,14 +219,17 @@ int main(int argc, char** argv) {
     if (argc >= 2 && std::string(argv[1]) == "bench")
         return benchMain(argc, argv);
     if (argc != 7 && argc != 8) {
-        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node|delayed|search]\n",
+        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node|delayed|search|late]\n",
                 argv[0]);
         return 2;
     }
     const std::string protocol = argc == 8 ? argv[7] : "recognizer";
-    if (protocol != "recognizer" && protocol != "node" && protocol != "delayed" && protocol != "search")
+    if (protocol != "recognizer" && protocol != "node" && protocol != "delayed" && protocol != "search" &&
+        protocol != "late")
         return 2;
     const bool search = protocol == "search";  // the recognizer's sequence, score(e) only (no bestDensity)
+    const bool late   = protocol == "late";    // score(e) only for the first half of the frames, then bestDensity too
+    uint32_t   consumed = 0;
     const bool     delayed = protocol == "delayed";
     const uint32_t kDelay  = 3;
     std::deque<Mm::Gpu::Scorer> pending;
@@ -281,10 +284,12 @@ int main(int argc, char** argv) {
     std::vector<float>    outS;
     std::vector<uint32_t> outB;
     auto consume = [&](const Mm::Gpu::Scorer& s) {  // the search reads score(e) for active e
-        const uint32_t n = node ? s->nEmissions() : M;  // the node dumps nEmissions() values per frame
+        const uint32_t n        = node ? s->nEmissions() : M;  // the node dumps nEmissions() values per frame
+        const bool     readBest = !search && (!late || 2 * consumed >= F) && s->hasBestDensity();
+        ++consumed;
         for (uint32_t e = 0; e < n; ++e) {
             outS.push_back(node ? -s->score(e) : s->score(e));  // FeatureScorerNode::putData: +log space
-            outB.push_back(!search && s->hasBestDensity() ? s->bestDensity(e) : 0xffffffffu);
+            outB.push_back(readBest ? s->bestDensity(e) : 0xffffffffu);
         }
     };
     const uint32_t segments = static_cast<uint32_t>(atoi(argv[6]));

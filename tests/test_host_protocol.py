@@ -250,3 +250,25 @@ def test_prefetch_then_best_densities(gpu, tmp_path, protocol):
     sign = -1.0 if protocol == "node" else 1.0
     assert np.array_equal((sign * s.T).astype(np.float32).view(np.uint32), ref_s.view(np.uint32))
     assert np.array_equal(b.T, ref_b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum"])
+def test_prefetch_then_late_best_densities(gpu, tmp_path, kind):
+    """score(e) only for the first half of the frames (prefetch runs, several asynchronous calls), then
+    bestDensity(e) as well: the best densities of positions whose call is no longer the newest come from one
+    refill of the buffer, and equal the oracle's (SIMD bit-exact; float: the scores within 1e-4, the best
+    densities where the two best candidates are not a near tie)."""
+    ms = ra.synthetic_mixture_set(30, 9, 39, seed=65, weights="random")
+    F = 400
+    frames = ra.synthetic_frames(F, 39, seed=66)
+    s, b, _ = _run(tmp_path, ms, frames, kind, 64, 1, protocol="late")
+    if kind == "SIMD-diagonal-maximum":
+        ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+        assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
+    else:
+        ref_s, ref_b = oracle.OracleFloat(ms).score(frames)
+        assert (np.abs(s.T.astype(np.float64) - ref_s) / np.maximum(1, np.abs(ref_s))).max() <= 1e-4
+    assert (b[: F // 2] == 0xFFFFFFFF).all()
+    agree = (b.T[:, F // 2:] == ref_b[:, F // 2:]).mean()
+    assert agree == 1.0 if kind == "SIMD-diagonal-maximum" else agree > 0.99
