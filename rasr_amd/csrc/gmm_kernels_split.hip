@@ -212,9 +212,6 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
 // loads (mixTileOff is a restrict kernel argument): a vector load there would come with an
 // s_waitcnt vmcnt(0) draining the prefetch.
 // ---------------------------------------------------------------------------
-#ifndef GMM_SPLIT_ROTATE
-#define GMM_SPLIT_ROTATE 1  // scoreSplit: per-frame-tile start mixture in the chunk (0: every workgroup from the first)
-#endif
 // PRESEL (preselection-batch-float): every key is OR-ed with the sign-extended mask byte of its
 // (frame, density cluster), so a density whose cluster the frame did not select becomes the all-ones
 // key and never wins; the wave's mask table (gmm_kernels_presel.hip) sits in LDS, a tile carries the
@@ -233,14 +230,8 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         return;
     const uint32_t frame0 = ft * kSplitFramesPerBlock + static_cast<uint32_t>(wave) * (NF * 16u);
     const uint32_t fb0    = frame0 / 16u;
-    const uint32_t cm0 = a.chunkMixOff[chunk], cm1 = a.chunkMixOff[chunk + 1];
-    // The chunk's mixtures are walked from a start that depends on the frame tile, wrapping around: workgroups of
-    // one chunk on the same CU (other frame tiles) then reach their mixture ends -- the emits -- at different
-    // times instead of in lockstep.  The chunk stays the L2 working set.
-    const uint32_t nmx = cm1 - cm0;
-    const uint32_t mS  = (GMM_SPLIT_ROTATE && nmx > 1) ? cm0 + ((ft * 2654435761u) >> 16) % nmx : cm0;
-    uint32_t       m0 = mS, m1 = cm1;  // the current pass: [mS, cm1), then [cm0, mS)
-    uint32_t       T0 = mixTileOff[m0], T1 = mixTileOff[m1];
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
 
     // preselection: this wave's 64-frame mask table [cluster][16] into LDS (each wave reads only its own)
     uint32_t laneSel = 0;  // byte address of (wave table, column t = lane & 15)
@@ -291,10 +282,13 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     }
     asm volatile("" ::"v"(eOut));
 
-    // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds (past a pass that ends
-    // inside the array: the next mixtures' tiles)
+    // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
     f16x8 R0[KS], R1[KS], R2[KS], R3[KS];
     uint2 C0{0, 0}, C1{0, 0}, C2{0, 0}, C3{0, 0};
+    loadTile(T0, R0, C0);
+    loadTile(T0 + 1, R1, C1);
+    loadTile(T0 + 2, R2, C2);
+    loadTile(T0 + 3, R3, C3);
 
     // scores only (no best density, no preselection mask): keys are the values' own bits, nothing masked
     const uint32_t kmask = (BEST || PRESEL) ? (1u << a.tileBits) - 1u : 0u;
@@ -414,18 +408,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         finish(tPrev + 2);
     };
 
-    for (int pass = 0; pass < 2; ++pass) {
-    if (pass == 1) {
-        if (mS == cm0)
-            break;
-        m0 = cm0, m1 = mS, T0 = mixTileOff[m0], T1 = mixTileOff[m1];
-        m = m0, tBeg = T0, tEnd = mixTileOff[m0 + 1];
-    }
-    loadTile(T0, R0, C0);
-    loadTile(T0 + 1, R1, C1);
-    loadTile(T0 + 2, R2, C2);
-    loadTile(T0 + 3, R3, C3);
-    // mixtures without tiles at the start of the pass
+    // mixtures without tiles at the start of the chunk
     while (m < m1 && tEnd == T0) {
         emit();
         ++m;
@@ -460,7 +443,6 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         else {
             drain(accX, t - 2, TTX);
         }
-    }
     }
 }
 
