@@ -1,6 +1,7 @@
 # Top-level build: the MI355X scorer library (HIP kernels + C-ABI + C++ host-side scorer
 # classes), the C++ protocol test driver, and the (test-only) oracle.  No cmake; hipcc for gfx950.
-HIPCC    ?= /opt/rocm/bin/hipcc
+ROCM_PATH ?= /opt/rocm
+HIPCC    ?= $(ROCM_PATH)/bin/hipcc
 ARCH     ?= gfx950
 BUILD     = build
 LIBDIR    = rasr_amd/lib
@@ -81,7 +82,7 @@ $(BUILD)/nn_api.o: $(SRC)/nn_api.cc $(HDRS)
 # summaries profiles/pmc_*.json measure), so a summary stays matched to the ISA it was collected on -- a source
 # edit that leaves the code unchanged keeps the id, any code change gives a new one; bench.py uses a summary
 # only for the kernels it was measured on
-BUNDLER   = /opt/rocm/lib/llvm/bin/clang-offload-bundler
+BUNDLER  ?= $(ROCM_PATH)/lib/llvm/bin/clang-offload-bundler
 KERNEL_OBJS = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o
 $(BUILD)/kernel_id.h: $(KERNEL_OBJS)
 	@for o in $(KERNEL_OBJS); do objcopy -O binary --only-section=.hip_fatbin $$o $$o.fatbin && \
@@ -120,7 +121,7 @@ $(BUILD)/MixtureSetEstimatorFile.o: $(SRC)/host/MixtureSetEstimatorFile.cc $(HDR
 
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz -pthread -lrccl
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz -pthread -ldl
 
 # host check of the score-only layout against the SCORE_ONLY kernel's arithmetic (no GPU)
 $(CLASSLAYOUT): tests/cpp/class_layout_test.cc $(BUILD)/gmm_prepare.o $(HDRS)
@@ -174,8 +175,39 @@ $(HARNESS): tests/rasr_harness/harness.cc tests/rasr_harness/gmm_standin.cc inte
 	    tests/rasr_harness/harness.cc tests/rasr_harness/gmm_standin.cc integration/rasr/Mm/GpuFeatureScorer.cc \
 	    $(SRC)/host/GpuFeatureScorer.cc -Loracle/_build -lgmm_oracle -Wl,-rpath,'$$ORIGIN/../../oracle/_build' -lm -pthread
 
-check-integration-link: $(HARNESS)
+# The hybrid-DNN adapter (all three integration/rasr/Nn files) linked and run the same way: test doubles of the Nn
+# network, prior and class-label classes (tests/rasr_harness/include/Nn), over an f32 stand-in of the NN C-ABI (CPU)
+# or the product library (GPU build, run by tests/test_nn_integration.py -m gpu)
+NN_ADAPTER = integration/rasr/Nn/GpuBatchFeatureScorer.cc integration/rasr/Nn/GpuBatchFeatureScorerNetwork.cc
+NN_HARNESS_DEPS = tests/rasr_harness/nn_harness.cc $(NN_ADAPTER) integration/rasr/Nn/GpuBatchFeatureScorer.hh \
+                  include/rasr_nn.h $(wildcard tests/rasr_harness/include/*/*.hh)
+NN_HARNESS_FLAGS = -std=c++17 -O1 -Wall -Wno-unused-variable -Itests/rasr_harness/include -Itests/rasr_harness/include/Nn -Iinclude
+NN_HARNESS = $(BUILD)/tests/rasr_nn_harness
+$(NN_HARNESS): $(NN_HARNESS_DEPS) tests/rasr_harness/nn_standin.cc
+	@mkdir -p $(BUILD)/tests
+	g++ $(NN_HARNESS_FLAGS) -o $@ tests/rasr_harness/nn_harness.cc $(NN_ADAPTER) tests/rasr_harness/nn_standin.cc -lm
+NN_HARNESS_GPU = $(BUILD)/tests/rasr_nn_harness_gpu
+$(NN_HARNESS_GPU): $(NN_HARNESS_DEPS) $(LIB)
+	@mkdir -p $(BUILD)/tests
+	g++ $(NN_HARNESS_FLAGS) -DHARNESS_PRODUCT -o $@ tests/rasr_harness/nn_harness.cc $(NN_ADAPTER) \
+	    -L$(LIBDIR) -lrasr_gmm -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -lm -pthread
+
+check-integration-link: $(HARNESS) $(NN_HARNESS)
 	$(HARNESS)
+
+# The same adapter + harness over the PRODUCT library (librasr_gmm.so: the HIP kernels and the host classes inside
+# it); the oracle is linked as the checker.  Built here, run on the GPU by tests/test_integration.py (-m gpu).
+HARNESS_GPU = $(BUILD)/tests/rasr_adapter_harness_gpu
+$(HARNESS_GPU): tests/rasr_harness/harness.cc integration/rasr/Mm/GpuFeatureScorer.cc integration/rasr/Mm/GpuFeatureScorer.hh \
+                $(SRC)/host/GpuFeatureScorer.hh $(wildcard tests/rasr_harness/include/*/*.hh) $(LIB) oracle
+	@mkdir -p $(BUILD)/tests
+	g++ -std=c++17 -O1 -Wall -Wno-unused-variable -DHARNESS_PRODUCT -Itests/rasr_harness/include -Iinclude -I$(SRC) -o $@ \
+	    tests/rasr_harness/harness.cc integration/rasr/Mm/GpuFeatureScorer.cc \
+	    -L$(LIBDIR) -lrasr_gmm -Loracle/_build -lgmm_oracle \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/_build' -lm -pthread
+
+# the harness binaries (variables defined above): built with everything else, so they travel to the GPU box
+all: $(HARNESS_GPU) $(NN_HARNESS) $(NN_HARNESS_GPU)
 
 clean:
 	rm -rf $(BUILD) $(LIBDIR)

@@ -104,6 +104,11 @@ typedef struct {
  * input, one v_min3 per two candidates (no density index to pack).  Same scores, bit for bit.  This flag
  * keeps the (score, density) key layout of SIMD-diagonal-maximum instead (A/B timing, tests). */
 #define GMM_FLAG_FULL_KEYS 16u
+/* SIMD-diagonal-maximum keeps, besides its key layout, a second copy of the quantized model on the score-only
+ * layout for calls without best densities (the search's score(e)); ~64 B per density more device memory.  The
+ * twin is best effort: if it cannot be built the scorer serves every call from the key layout.  This flag skips
+ * it (callers that always ask for best densities, e.g. aligners). */
+#define GMM_FLAG_NO_SCORE_ONLY_TWIN 32u
 
 typedef struct gmm_scorer gmm_scorer;
 

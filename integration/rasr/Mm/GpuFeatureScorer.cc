@@ -14,9 +14,9 @@ using namespace Mm;
 
 const Core::ParameterInt GpuFeatureScorer::paramBufferSize(
         "buffer-size",
-        "frames scored per GPU launch (1: every frame on its own, unbuffered); default 512, the measured throughput knee "
-        "(online decoding: 1..4)",
-        512, 1);
+        "frames scored per GPU launch (1: every frame on its own, unbuffered); default 4 as the reference batch "
+        "scorers (BatchFeatureScorer.cc:28-29); 512 is the measured throughput knee for offline recognition",
+        4, 1);
 const Core::ParameterInt GpuFeatureScorer::paramDevice(
         "device", "HIP device of this process (one process per GPU)", 0, 0);
 const Core::ParameterIntVector GpuFeatureScorer::paramShardDevices(

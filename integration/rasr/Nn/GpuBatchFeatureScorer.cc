@@ -98,28 +98,38 @@ Mm::FeatureScorer::Scorer GpuBatchFeatureScorer::getScorer(const Mm::FeatureVect
     return scorer;
 }
 
+// BatchFeatureScorer::flush (cc:119-134).  Deliberate deviation: the reference clears the feature buffer when the
+// last buffered frame is flushed, BEFORE that frame's context is read; when the frame was added after the last
+// forward pass (its scores not computed yet) the reference then scores an all-zero frame for it.  Here the pending
+// scores are computed first, so the last frame of a segment scores its own features.
 Mm::FeatureScorer::Scorer GpuBatchFeatureScorer::flush() const {
     require(!bufferEmpty());
-    Scorer scorer(new ContextScorer(this, currentFeature_));
+    const u32 position = currentFeature_;
+    Scorer    scorer(new ContextScorer(this, position));
     currentFeature_ = (currentFeature_ + 1) % bufferSize_;
     nBufferedFeatures_--;
     if (bufferEmpty()) {
+        if (!scoreComputed_[position])
+            computeScores();
         currentFeature_ = 0;
         std::memset(buffer_, 0, static_cast<size_t>(bufferSize_) * inputDimension_ * sizeof(float));
     }
     return scorer;
 }
 
+// the whole buffer in one call (network_.forward(buffer_), cc:155-163)
+void GpuBatchFeatureScorer::computeScores() const {
+    if (nn_score_host_ex(scorer_, buffer_, bufferSize_, inputDimension_, scores_, nOutputs_, NN_HOST_FRAME_MAJOR) != GMM_OK)
+        criticalError("GPU nn scorer: %s", nn_last_error());
+    scoreComputed_.assign(bufferSize_, true);
+}
+
 // BatchFeatureScorer::getScore (cc:148-171): the whole buffer in one call when a position is out of date
 Mm::Score GpuBatchFeatureScorer::getScore(Mm::EmissionIndex e, u32 position) const {
     require_lt(position, bufferSize_);
     require_lt(e, nClasses_);
-    if (!scoreComputed_[position]) {
-        if (nn_score_host_ex(scorer_, buffer_, bufferSize_, inputDimension_, scores_, nOutputs_, NN_HOST_FRAME_MAJOR) !=
-            GMM_OK)
-            criticalError("GPU nn scorer: %s", nn_last_error());
-        scoreComputed_.assign(bufferSize_, true);
-    }
+    if (!scoreComputed_[position])
+        computeScores();
     if (outputIndex_[e] < 0)  // !labelWrapper_->isClassToAccumulate(e)
         return Core::Type<Mm::Score>::max;
     // the table holds -output (nn_score_*: score = -(W^T h + b)), the reference's -getTopLayerOutput().at(e, position)

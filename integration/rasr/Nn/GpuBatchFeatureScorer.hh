@@ -69,7 +69,7 @@ public:
     virtual void addFeature(Core::Ref<const Mm::Feature> f) const {
         addFeature(*f->mainStream());
     }
-    virtual FeatureScorer::Scorer flush() const;  // cc:119-134
+    virtual FeatureScorer::Scorer flush() const;  // cc:119-134 (scores a pending last frame before clearing)
     virtual bool                  bufferFilled() const {
         return nBufferedFeatures_ >= bufferSize_ - 1;
     }
@@ -86,6 +86,7 @@ private:
     // upload (GpuBatchFeatureScorerNetwork.cc): sets nClasses_, inputDimension_, nOutputs_, outputIndex_, scorer_
     void initNetwork(Core::Ref<const Mm::MixtureSet> mixtureSet);
     void setFeature(u32 position, const Mm::FeatureVector& f) const;
+    void computeScores() const;  // every buffer position in one nn_score_host_ex call
 
     const u32                 bufferSize_;
     mutable u32               nBufferedFeatures_;

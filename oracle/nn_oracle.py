@@ -71,11 +71,12 @@ def forward_bf16(layers, frames, log_prior=None, prior_scale=1.0):
 
 
 def prior_from_mixture_set(ms) -> np.ndarray:
-    """Prior::setFromMixtureSet: f32 per-mixture weight sums, normalized by their f64-accumulated
-    total (std::accumulate with a 0.0 init), std::log."""
+    """Prior::setFromMixtureSet: f32 per-mixture weight sums (`f32 += Mm::Weight`, an f64 (src/Mm/Types.hh:30):
+    the sum formed in f64 and rounded to f32 per density), normalized by their f64-accumulated total
+    (std::accumulate with a 0.0 init), std::log."""
     p = np.zeros(ms.n_mixtures, np.float32)
     for m in range(ms.n_mixtures):
         for i in range(int(ms.mixture_offsets[m]), int(ms.mixture_offsets[m + 1])):
-            p[m] = np.float32(p[m] + np.float32(np.exp(ms.mixture_log_weights[i])))
+            p[m] = np.float32(np.float64(p[m]) + np.exp(np.float64(ms.mixture_log_weights[i])))
     total = np.float32(sum(float(v) for v in p))
     return np.log(p / total).astype(np.float32)

@@ -19,6 +19,7 @@ GMM_FLAG_SPLIT_TILE16 = 2
 GMM_FLAG_SPLIT_TILE32 = 4
 GMM_FLAG_REFERENCE_ORDER = 8  # diagonal-maximum / batch-float in the reference's f32 operation order
 GMM_FLAG_FULL_KEYS = 16  # batch-int / -fast: (score, density) keys instead of the score-only class layout
+GMM_FLAG_NO_SCORE_ONLY_TWIN = 32  # SIMD: no score-only copy of the model (callers that always want best densities)
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0

@@ -6,8 +6,9 @@
 // stream: the frame preparation (quantize / scale the feature vectors, the
 // per-frame Context of the reference, SimdFeatureScorer.cc:22-35) and the
 // scorer.  No host synchronisation, no allocation on that path.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
+#include <rccl/rccl.h>  // types only: the library is opened at run time (Rccl below)
 
 #include <algorithm>
 #include <cstdio>
@@ -43,6 +44,47 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                                       \
             return fail(GMM_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));        \
     } while (0)
+
+// RCCL, opened on first use by a density-sharded handle with the RCCL exchange: single-GPU users of the library
+// need no RCCL installation, and the library has no link-time dependency on it
+struct Rccl {
+    ncclResult_t (*commInitAll)(ncclComm_t*, int, const int*)                                           = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t)                                                             = nullptr;
+    ncclResult_t (*allReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*groupStart)()                                                                        = nullptr;
+    ncclResult_t (*groupEnd)()                                                                          = nullptr;
+    const char* (*errorString)(ncclResult_t)                                                            = nullptr;
+    std::string error;  // empty: loaded
+};
+
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void*                    h = nullptr;
+        std::vector<std::string> names{"librccl.so.1", "librccl.so"};
+        if (const char* rocm = std::getenv("ROCM_PATH"))
+            names.push_back(std::string(rocm) + "/lib/librccl.so.1");
+        names.push_back("/opt/rocm/lib/librccl.so.1");
+        for (const std::string& name : names)
+            if ((h = dlopen(name.c_str(), RTLD_NOW | RTLD_GLOBAL)))
+                break;
+        if (!h) {
+            const char* e = dlerror();
+            x.error = std::string("cannot open librccl.so.1: ") + (e ? e : "?");
+            return x;
+        }
+        x.commInitAll = reinterpret_cast<decltype(x.commInitAll)>(dlsym(h, "ncclCommInitAll"));
+        x.commDestroy = reinterpret_cast<decltype(x.commDestroy)>(dlsym(h, "ncclCommDestroy"));
+        x.allReduce   = reinterpret_cast<decltype(x.allReduce)>(dlsym(h, "ncclAllReduce"));
+        x.groupStart  = reinterpret_cast<decltype(x.groupStart)>(dlsym(h, "ncclGroupStart"));
+        x.groupEnd    = reinterpret_cast<decltype(x.groupEnd)>(dlsym(h, "ncclGroupEnd"));
+        x.errorString = reinterpret_cast<decltype(x.errorString)>(dlsym(h, "ncclGetErrorString"));
+        if (!x.commInitAll || !x.commDestroy || !x.allReduce || !x.groupStart || !x.groupEnd || !x.errorString)
+            x.error = "librccl.so lacks an nccl* entry point";
+        return x;
+    }();
+    return r;
+}
 
 template <class T>
 int upload(T** dst, const std::vector<T>& src, size_t padElems = 0) {
@@ -833,8 +875,11 @@ int scoreHost(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, u
 //   every part, on its own stream after S's start event: frames -> its device (peer copy; none on devices[0]),
 //     its sub-model scored into [nLocal][n], the split mixtures it holds packed into keys [nSplit][n]
 //     (INT64_MAX for the ones it does not hold), then
-//   the per-frame reduce of the keys: RCCL all-reduce(MIN) over all parts (ncclGroupStart/End, one comm per
-//     GPU), or peer copies of every part's keys to devices[0] and minShardKeys there;
+//   the per-frame reduce of the keys, either
+//     RCCL: on every GPU the keys of its other parts folded into its first part's (minIntoShardKeys), then an
+//       all-reduce(MIN) over those first parts, one rank per distinct GPU (ncclGroupStart/End, one comm per GPU);
+//       with every part on one GPU that is a one-rank all-reduce, which is how a one-GPU box runs this path, or
+//     COPY: peer copies of every part's keys to devices[0] and minShardKeys there;
 //   every part copies its whole mixtures (local rows [rowLo, rowHi)) into the full table's rows;
 //   S waits for every part, unpacks the split mixtures' keys into their rows.
 // The full table's other rows come straight from the parts: no all-gather (the caller reads one table).
@@ -849,6 +894,8 @@ struct DensityPart {
     uint32_t*    dHeldOffset = nullptr;                        // [held] in-mixture index of the row's first entry
     hipStream_t  stream      = nullptr;
     hipEvent_t   done        = nullptr;
+    hipEvent_t   keysReady   = nullptr;  // RCCL: this part's keys packed (parts other than their GPU's first)
+    std::vector<uint32_t> fold;          // RCCL: the other parts on this part's GPU (this part is their first)
     float*       dFrames     = nullptr;  // [maxF][D] (parts not on devices[0])
     float*       dScores     = nullptr;  // [nLocal][maxF]
     uint32_t*    dBest       = nullptr;
@@ -859,7 +906,8 @@ struct DensityGroup {
     std::vector<DensityPart> parts;
     std::vector<uint32_t>    split;  // mixtures held by more than one part
     int                      exchange = GMM_EXCHANGE_AUTO;
-    std::vector<ncclComm_t>  comms;
+    std::vector<uint32_t>    ranks;  // RCCL: the first part on each distinct GPU, in device-list order
+    std::vector<ncclComm_t>  comms;  // RCCL: one per entry of ranks
     int                      lead     = 0;        // devices[0]
     int64_t*                 dGather  = nullptr;  // COPY: [parts][nSplit][maxF] on the lead
     int64_t*                 dReduced = nullptr;  // COPY: [nSplit][maxF]
@@ -874,15 +922,16 @@ struct DensityGroup {
         }
         for (ncclComm_t c : comms)
             if (c)
-                (void)ncclCommDestroy(c);
+                (void)rccl().commDestroy(c);
         for (DensityPart& p : parts) {
             (void)hipSetDevice(p.device);
             for (void* q : {static_cast<void*>(p.dHeldOffset), static_cast<void*>(p.dFrames), static_cast<void*>(p.dScores),
                             static_cast<void*>(p.dBest), static_cast<void*>(p.dKeys)})
                 if (q)
                     (void)hipFree(q);
-            if (p.done)
-                (void)hipEventDestroy(p.done);
+            for (hipEvent_t ev : {p.done, p.keysReady})
+                if (ev)
+                    (void)hipEventDestroy(ev);
             if (p.stream)
                 (void)hipStreamDestroy(p.stream);
             if (p.scorer)
@@ -904,7 +953,7 @@ namespace {
     do {                                                                                            \
         ncclResult_t r_ = (expr);                                                                   \
         if (r_ != ncclSuccess)                                                                      \
-            return fail(GMM_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_));        \
+            return fail(GMM_ERR_DEVICE, std::string(#expr) + ": " + rccl().errorString(r_));      \
     } while (0)
 
 int groupScore(gmm_scorer* s, const float* frames, uint32_t n, uint32_t frameStride, float* scores, uint32_t* best,
@@ -938,25 +987,38 @@ int groupScore(gmm_scorer* s, const float* frames, uint32_t n, uint32_t frameStr
                                                   p.dHeldOffset + h, 1, n, n, p.dKeys + static_cast<size_t>(slot) * n,
                                                   p.stream));
             }
+            if (p.keysReady)
+                GMM_HIP_CHECK(hipEventRecord(p.keysReady, p.stream));
         }
     }
     // the per-frame reduce of the split mixtures
     const int64_t* reduced = nullptr;
     if (nS && g.exchange == GMM_EXCHANGE_RCCL) {
-        GMM_NCCL_CHECK(ncclGroupStart());
+        // on every GPU: its other parts' keys folded into its first part's, on that part's stream
+        for (uint32_t r : g.ranks) {
+            DensityPart& lead = g.parts[r];
+            GMM_HIP_CHECK(hipSetDevice(lead.device));
+            for (uint32_t f : lead.fold) {
+                GMM_HIP_CHECK(hipStreamWaitEvent(lead.stream, g.parts[f].keysReady, 0));
+                GMM_HIP_CHECK(launchMinIntoShardKeys(lead.dKeys, g.parts[f].dKeys, keyN, lead.stream));
+            }
+        }
+        // across GPUs: all-reduce(MIN) in place, one rank per GPU
+        const Rccl& x = rccl();
+        GMM_NCCL_CHECK(x.groupStart());
         ncclResult_t nr = ncclSuccess;
         hipError_t   hr = hipSuccess;
-        for (uint32_t i = 0; i < P && nr == ncclSuccess && hr == hipSuccess; ++i) {
-            DensityPart& p = g.parts[i];
+        for (size_t i = 0; i < g.ranks.size() && nr == ncclSuccess && hr == hipSuccess; ++i) {
+            DensityPart& p = g.parts[g.ranks[i]];
             if ((hr = hipSetDevice(p.device)) == hipSuccess)
-                nr = ncclAllReduce(p.dKeys, p.dKeys, keyN, ncclInt64, ncclMin, g.comms[i], p.stream);
+                nr = x.allReduce(p.dKeys, p.dKeys, keyN, ncclInt64, ncclMin, g.comms[i], p.stream);
         }
-        const ncclResult_t ne = ncclGroupEnd();  // always closes the group, also after a failed enqueue
+        const ncclResult_t ne = x.groupEnd();  // always closes the group, also after a failed enqueue
         if (hr != hipSuccess)
             return fail(GMM_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(hr));
         GMM_NCCL_CHECK(nr);
         GMM_NCCL_CHECK(ne);
-        reduced = g.parts[0].dKeys;  // part 0 is on the lead device
+        reduced = g.parts[0].dKeys;  // part 0 is the first part on the lead device
     }
     else if (nS) {
         for (uint32_t i = 0; i < P; ++i) {
@@ -1227,11 +1289,16 @@ int gmm_scorer_create(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm
     gmm_scorer* s = *out;
     if (s->multiCov || s->kSteps != 1)
         return GMM_OK;  // the class layout covers one covariance and D <= 64 (the key layout serves the rest)
+    if (s->cfg.flags & GMM_FLAG_NO_SCORE_ONLY_TWIN)
+        return GMM_OK;  // callers that always ask for best densities (aligners): no second copy of the model
+    // best effort: the twin only speeds up calls without best densities, so a twin that cannot be built (e.g. the
+    // device has no room for a second copy of the model) leaves a valid scorer on the key layout
     gmm_scorer* twin = nullptr;
-    if ((rc = createScorer(ms, type, &s->cfg, device, true, &twin)) != GMM_OK) {
-        gmm_scorer_destroy(s);
-        *out = nullptr;
-        return rc;
+    if (createScorer(ms, type, &s->cfg, device, true, &twin) != GMM_OK) {
+        (void)hipGetLastError();
+        (void)hipSetDevice(device);
+        gLastError.clear();
+        return GMM_OK;
     }
     if (twin->scoreOnly)
         s->scoresOnly.reset(twin);
@@ -1263,15 +1330,9 @@ int gmm_scorer_create_sharded(const gmm_mixture_set* ms, gmm_scorer_type type, c
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(GMM_ERR_DEVICE, "no HIP device available");
-    bool distinct = true;
-    for (uint32_t i = 0; i < nDevices; ++i) {
+    for (uint32_t i = 0; i < nDevices; ++i)
         if (devices[i] < 0 || devices[i] >= ndev)
             return fail(GMM_ERR_INVALID_ARGUMENT, "device index out of range");
-        for (uint32_t j = 0; j < i; ++j)
-            distinct = distinct && devices[j] != devices[i];
-    }
-    if (exchange == GMM_EXCHANGE_RCCL && !distinct)
-        return fail(GMM_ERR_UNSUPPORTED, "the RCCL exchange needs distinct devices (one rank per GPU); use GMM_EXCHANGE_COPY");
     if (nDevices == 1)  // the unsharded scorer itself
         return gmm_scorer_create(ms, type, &cfg, devices[0], out);
 
@@ -1282,8 +1343,16 @@ int gmm_scorer_create_sharded(const gmm_mixture_set* ms, gmm_scorer_type type, c
     std::unique_ptr<DensityGroup> g(new DensityGroup);
     g->split = splitMixtures(plan);
     g->lead  = devices[0];
+    // AUTO: RCCL when the parts span several GPUs, the on-device copy exchange when they share one
+    std::vector<int> gpus;
+    for (uint32_t i = 0; i < nDevices; ++i)
+        if (std::find(gpus.begin(), gpus.end(), devices[i]) == gpus.end())
+            gpus.push_back(devices[i]);
     g->exchange = g->split.empty() ? GMM_EXCHANGE_AUTO
-                                   : (exchange == GMM_EXCHANGE_AUTO ? (distinct ? GMM_EXCHANGE_RCCL : GMM_EXCHANGE_COPY) : exchange);
+                                   : (exchange == GMM_EXCHANGE_AUTO ? (gpus.size() > 1 ? GMM_EXCHANGE_RCCL : GMM_EXCHANGE_COPY)
+                                                                    : exchange);
+    if (g->exchange == GMM_EXCHANGE_RCCL && !rccl().error.empty())
+        return fail(GMM_ERR_UNSUPPORTED, "the RCCL exchange: " + rccl().error);
     const size_t maxF = cfg.max_frames, nS = g->split.size();
     const auto   isSplit = [&](uint32_t m) { return std::binary_search(g->split.begin(), g->split.end(), m); };
     g->parts.resize(nDevices);
@@ -1348,8 +1417,21 @@ int gmm_scorer_create_sharded(const gmm_mixture_set* ms, gmm_scorer_type type, c
         }
     }
     if (g->exchange == GMM_EXCHANGE_RCCL) {
-        g->comms.assign(nDevices, nullptr);
-        GMM_NCCL_CHECK(ncclCommInitAll(g->comms.data(), static_cast<int>(nDevices), devices));
+        // one rank per GPU: the first part on each GPU; the others fold their keys into it first
+        for (int d : gpus)
+            for (uint32_t r = 0; r < nDevices; ++r)
+                if (devices[r] == d) {
+                    g->ranks.push_back(r);
+                    for (uint32_t f = r + 1; f < nDevices; ++f)
+                        if (devices[f] == d) {
+                            g->parts[r].fold.push_back(f);
+                            GMM_HIP_CHECK(hipSetDevice(d));
+                            GMM_HIP_CHECK(hipEventCreateWithFlags(&g->parts[f].keysReady, hipEventDisableTiming));
+                        }
+                    break;
+                }
+        g->comms.assign(gpus.size(), nullptr);
+        GMM_NCCL_CHECK(rccl().commInitAll(g->comms.data(), static_cast<int>(gpus.size()), gpus.data()));
     }
     GMM_HIP_CHECK(hipSetDevice(g->lead));
     if (g->exchange == GMM_EXCHANGE_COPY) {

@@ -186,6 +186,8 @@ hipError_t launchUnpackShardKeys(const int64_t* keys, uint32_t rows, uint32_t nF
                                  uint32_t stride, hipStream_t stream);
 hipError_t launchFillShardKeys(int64_t* keys, size_t n, hipStream_t stream);  // keys[i] = INT64_MAX
 hipError_t launchMinShardKeys(const int64_t* slots, uint32_t nSlots, size_t n, int64_t* out, hipStream_t stream);
+// dst[i] = min(dst[i], src[i]): the device-local fold of the RCCL exchange (parts that share a GPU)
+hipError_t launchMinIntoShardKeys(int64_t* dst, const int64_t* src, size_t n, hipStream_t stream);
 
 // frame-major host tables (gmm_kernels_layout.hip): dst[c * dstPitch + r] = src[r * srcPitch + c], 32-bit words
 hipError_t launchTransposeWords(const uint32_t* src, uint32_t rows, uint32_t cols, uint32_t srcPitch, uint32_t* dst,

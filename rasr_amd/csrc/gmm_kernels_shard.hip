@@ -77,6 +77,14 @@ __global__ __launch_bounds__(256) void minShardKeys(const int64_t* __restrict__ 
     out[i] = k;
 }
 
+// the device-local fold of the RCCL exchange: another part's keys on the same GPU into the GPU's first part's
+__global__ __launch_bounds__(256) void minIntoShardKeys(int64_t* __restrict__ dst, const int64_t* __restrict__ src,
+                                                        size_t n) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n)
+        dst[i] = min(dst[i], src[i]);
+}
+
 }  // namespace dev
 
 hipError_t launchPackShardKeys(const float* scores, const uint32_t* best, const uint32_t* bestOffset, uint32_t rows,
@@ -111,6 +119,14 @@ hipError_t launchMinShardKeys(const int64_t* slots, uint32_t nSlots, size_t n, i
         return hipSuccess;
     hipLaunchKernelGGL(dev::minShardKeys, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, stream, slots,
                        nSlots, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launchMinIntoShardKeys(int64_t* dst, const int64_t* src, size_t n, hipStream_t stream) {
+    if (n == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(dev::minIntoShardKeys, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, stream, dst, src,
+                       n);
     return hipGetLastError();
 }
 

@@ -219,11 +219,16 @@ public:
     BufferedScorer(const GpuBatchFeatureScorer* parent, uint32_t currentFeature, uint32_t buffered, bool assigning)
             : parent_(parent), currentFeature_(currentFeature), buffered_(buffered), assigning_(assigning) {}
     EmissionIndex nEmissions() const override { return parent_->nMixtures(); }
-    // the first score(e) fills the position if needed and keeps its row of the frame-major table: the row stays
-    // valid while the context is (the protocol reuses the position only at a later getScorer())
+    // the first score(e) fills the position if needed and keeps its row of the frame-major table.  A later
+    // getScorer() may reuse the position for a new frame (and a prefetch may then be writing that row): the
+    // generation check sends such a context back through scoreRow(), which lands the call in flight first --
+    // the reference's getScore() likewise answers from the position's current fill
     Score score(EmissionIndex e) const override {
-        if (!row_)
+        const uint32_t g = parent_->positionGeneration(currentFeature_);
+        if (!row_ || g != gen_) {
             row_ = parent_->scoreRow(currentFeature_, buffered_);
+            gen_ = g;
+        }
         return row_[e];
     }
     bool             hasBestDensity() const override { return assigning_; }
@@ -236,6 +241,7 @@ private:
     uint32_t                     currentFeature_, buffered_;
     bool                         assigning_;
     mutable const float*         row_ = nullptr;
+    mutable uint32_t             gen_ = 0;
 };
 
 }  // namespace
@@ -334,6 +340,7 @@ std::unique_ptr<GpuBatchFeatureScorer> GpuBatchFeatureScorer::create(const Mixtu
         return nullptr;
     }
     s->cached_.assign(b, 0);
+    s->generation_.assign(b, 0);
     s->bestCached_.assign(b, 0);
     s->bestCall_.assign(b, 0);
     s->inflight_.assign(b, 0);
@@ -353,6 +360,8 @@ void GpuBatchFeatureScorer::reset() const {
     asyncCall_ = 0;
     std::fill(inflight_.begin(), inflight_.end(), 0);
     std::fill(cached_.begin(), cached_.end(), 0);
+    for (uint32_t& g : generation_)
+        ++g;
     pendingCount_   = 0;
     currentFeature_ = 0;
     buffered_       = 0;
@@ -363,6 +372,7 @@ void GpuBatchFeatureScorer::setFeature(size_t pos, const FeatureVector& f) const
     if (inflight_[pos])  // its row may not have been read yet (a context whose scores were never asked for)
         landInflight();
     std::copy(f.begin(), f.end(), features_.data() + pos * dimension_);
+    ++generation_[pos];
     if (!prefetchChunk_ || bestWanted_)
         return;
     // the new frame joins the pending run (it is the newest buffered position)

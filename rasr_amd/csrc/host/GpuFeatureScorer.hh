@@ -218,6 +218,10 @@ public:
     // the scores of every emission of the buffered position featureIndex (filled first if needed): nMixtures()
     // floats of the page-locked frame-major table, valid until the protocol reuses the position
     const float*     scoreRow(uint32_t featureIndex, uint32_t length) const;
+    // changes whenever the position of featureIndex takes a new frame (or the ring is reset): a context that keeps
+    // a scoreRow() pointer re-reads through scoreRow() once the generation moved, so it never reads a row that an
+    // asynchronous call is still writing
+    uint32_t         positionGeneration(uint32_t featureIndex) const { return generation_[featureIndex % bufferSize_]; }
     // 0xffffffff for the batch types, which have no assignment (as ContextScorer::bestDensity)
     DensityInMixture getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
 
@@ -247,6 +251,7 @@ private:
     HostTable<uint32_t>       best_;
     mutable std::vector<float> scratch_;     // [nMixtures] scores of a re-scored position (not kept)
     mutable std::vector<char> cached_;       // [bufferSize] scores of the position are in scores_
+    mutable std::vector<uint32_t> generation_; // [bufferSize] frames the position has taken (positionGeneration)
     mutable std::vector<char> bestCached_;   // [bufferSize] best densities of the position are in best_
     mutable std::vector<uint64_t> bestCall_; // [bufferSize] host call that scored the position
     // Prefetch (buffers of kPrefetchMin frames and more): the newest frames not yet scored (pending: the ring run

@@ -119,12 +119,13 @@ const char* nn_last_error(void) {
 int nn_prior_from_mixture_set(const gmm_mixture_set* ms, float* logPrior) {
     if (!ms || !logPrior || !ms->mixture_offsets || !ms->mixture_log_weights)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
-    // Prior::setFromMixtureSet (src/Nn/Prior.cc:159-190): f32 sums of mixture->weight(dns) = exp(logw),
+    // Prior::setFromMixtureSet (src/Nn/Prior.cc:159-190): f32 sums of mixture->weight(dns) = exp(logw), an f64
+    // (Mm::Weight, src/Mm/Types.hh:30): `f32 += f64` adds in f64 and rounds the sum to f32 once per density;
     // normalized by their (double-accumulated, std::accumulate with 0.0) total, then std::log
     std::vector<float> p(ms->n_mixtures, 0.0f);
     for (uint32_t m = 0; m < ms->n_mixtures; ++m)
         for (uint32_t i = ms->mixture_offsets[m]; i < ms->mixture_offsets[m + 1]; ++i)
-            p[m] += static_cast<float>(std::exp(ms->mixture_log_weights[i]));
+            p[m] = static_cast<float>(static_cast<double>(p[m]) + std::exp(ms->mixture_log_weights[i]));
     double total = 0.0;
     for (float v : p)
         total += v;

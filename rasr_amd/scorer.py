@@ -35,7 +35,8 @@ class Scorer:
                  score_scale: float = 1.0, mixture_range: tuple[int, int] | None = None, native_f32: bool = False,
                  split_tile16: bool = False, split_tile32: bool = False, clusters: int = 256,
                  select_clusters: int = 32, clustering_iterations: int = 5, backoff_score: float = 40000.0,
-                 reference_order: bool = False, devices=None, exchange: str = "auto", full_keys: bool = False):
+                 reference_order: bool = False, devices=None, exchange: str = "auto", full_keys: bool = False,
+                 no_score_only_twin: bool = False):
         self._lib = _capi.load_library()
         self.mixture_set = mixture_set
         self.type = _type_id(scorer_type)
@@ -54,6 +55,8 @@ class Scorer:
             cfg.flags |= _capi.GMM_FLAG_REFERENCE_ORDER
         if full_keys:  # batch-int / -fast: the (score, density) key layout instead of the score-only one
             cfg.flags |= _capi.GMM_FLAG_FULL_KEYS
+        if no_score_only_twin:  # SIMD: serve calls without best densities from the key layout too
+            cfg.flags |= _capi.GMM_FLAG_NO_SCORE_ONLY_TWIN
         # density preselection ("density-clustering" parameters, preselection-batch-* types)
         cfg.clusters = int(clusters)
         cfg.select_clusters = int(select_clusters)

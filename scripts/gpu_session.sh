@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU session on the gpurun box: each step under its own time limit, stop at the first failure.
+#   RUN=<name> STEPS="pytest smoke bench prof" scripts/gpu_session.sh
+# Outputs under gpurun_out/$RUN/ (copy what is to be kept into profiles/).
+#   pytest  : the -m gpu suite (PYTEST_ARGS overrides the selection, e.g. "tests/test_rccl_exchange.py")
+#   smoke   : __graft_entry__.smoke()
+#   bench   : python bench.py (BENCH_ARGS appended)
+#   prof    : rocprofv3 --kernel-trace --stats over bench.py (BENCH_ARGS appended)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${RUN:-session}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-pytest smoke}; do
+  case $s in
+    pytest) step pytest 1100 python -u -m pytest ${PYTEST_ARGS:-tests -m gpu} -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  step bench 900 python bench.py ${BENCH_ARGS} ;;
+    prof)   step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py ${BENCH_ARGS} ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done

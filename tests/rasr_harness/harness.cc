@@ -1,6 +1,9 @@
 // harness.cc -- TEST INFRASTRUCTURE ONLY: the RASR-side adapter (integration/rasr/Mm/GpuFeatureScorer.cc) linked
-// and run on the CPU inside test doubles of RASR's plugin machinery (tests/rasr_harness/include/README), over the
-// oracle-backed C-ABI stand-in (gmm_standin.cc) and the real host-side classes (rasr_amd/csrc/host).
+// and run inside test doubles of RASR's plugin machinery (tests/rasr_harness/include/README) together with the real
+// host-side classes (rasr_amd/csrc/host), in two builds (Makefile):
+//   rasr_adapter_harness      (CPU)  over the oracle-backed C-ABI stand-in (gmm_standin.cc);
+//   rasr_adapter_harness_gpu  (GPU, -DHARNESS_PRODUCT) over the PRODUCT library librasr_gmm.so -- the HIP kernels;
+//                                    the oracle is linked as the checker only.
 //
 //   1. Mm::registerGpuFeatureScorers(0x500) registers "gpu-<type>" with Mm::Module's FeatureScorerFactory
 //      (src/Mm/FeatureScorerFactory.hh:54-66); the scorer is created by id from a configuration whose
@@ -8,15 +11,23 @@
 //      acoustic model does (src/Mm/ScaledFeatureScorer.hh:56-153; scale 0.75).
 //   2. Speech::OfflineRecognizer's sequence (src/Speech/Recognizer.cc:272-282 processFeature with
 //      Core::Ref<const Feature>, :198-206 leaveSpeechSegment, reset per segment): every fed context is read
-//      for all emissions, and (assigning types) bestDensity(e) on the unscaled context.
+//      for all emissions -- once as the search does (score(e) only, SearchSpace.cc:1613-1659), and for the
+//      assigning types once as an aligner does (score(e) and bestDensity(e) on the unscaled context,
+//      AlignmentNode.cc:283-310).
 //   3. Speech::FeatureScorerNode::work (src/Speech/FeatureScorerNode.cc:113-162): -score(e) of all nEmissions()
 //      per frame, flush until empty, finalize(), reset().
-// Expected values: the oracle on all frames at once, the scaled score 0.75f * score.  Exit 0 = every check passed.
-// A forked child also checks that the adapter's criticalError routing aborts with the component's message when
-// bestDensity() is asked of a type without assignments.
+//   Buffer sizes 1, 4, 64 and 512 (64 and 512: the ring's asynchronous prefetch), "density-shard-devices".
+// Expected values: the oracle on all frames at once, the scaled score 0.75f * score.  SIMD-diagonal-maximum and
+// batch-diagonal-maximum-int: bit for bit.  Float types: bit for bit against the stand-in (it IS the oracle); against
+// the product library within the float contract, |got - want| <= 1e-4 max(1, |want|), and a different best density
+// only where both densities' f64 scores agree within that tolerance.  Exit 0 = every check
+// passed.  The CPU build also checks, in a forked child, that the adapter's criticalError routing aborts with the
+// component's message when bestDensity() is asked of a type without assignments (the GPU build does not fork a
+// process that may hold a GPU context; the routing is the adapter's own code, the same in both builds).
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -93,6 +104,25 @@ Model makeModel(uint32_t D, uint32_t M, uint64_t seed) {
     return m;
 }
 
+#ifdef HARNESS_PRODUCT
+constexpr bool kProduct = true;
+#else
+constexpr bool kProduct = false;
+#endif
+
+// f64 score of entry j of mixture e for frame x (GaussDiagonalMaximumFeatureScorer, defaults mws = gs = 1:
+// 0.5 (-2 log c + D log 2pi + sum log var + sum ((mu - x) / sigma)^2)), for the near-tie check of float best densities
+double f64Score(const Model& m, const float* x, uint32_t e, uint32_t j) {
+    const uint32_t D = m.ms->dimension(), entry = m.off[e] + j;
+    const float*   mu = &m.means[static_cast<size_t>(m.dMean[m.dens[entry]]) * D];
+    double         q = -2.0 * m.logw[entry] + D * std::log(2.0 * M_PI);
+    for (uint32_t k = 0; k < D; ++k) {
+        const double v = m.vars[k], d = (static_cast<double>(mu[k]) - x[k]);
+        q += std::log(v) + d * d / v;
+    }
+    return 0.5 * q;
+}
+
 int gFailures = 0;
 void check(bool ok, const std::string& what) {
     if (!ok) {
@@ -104,7 +134,14 @@ void check(bool ok, const std::string& what) {
 struct Expected {
     std::vector<float>    s;  // [M][F]
     std::vector<uint32_t> b;
+    bool                  exact = true;  // false: the float contract (product library, float types)
 };
+
+bool sameScore(float want, float got, bool exact) {
+    if (exact || !std::isfinite(want))
+        return std::memcmp(&want, &got, sizeof(float)) == 0;  // bit for bit (and the "no score" values exactly)
+    return std::fabs(static_cast<double>(got) - want) <= 1e-4 * std::max(1.0, std::fabs(static_cast<double>(want)));
+}
 
 Expected oracleScores(const Model& m, const std::string& type, const std::vector<float>& frames, uint32_t F) {
     const orc_mixture_set ms = m.view();
@@ -128,6 +165,7 @@ Expected oracleScores(const Model& m, const std::string& type, const std::vector
         orc_batch_int_score(&ms, frames.data(), F, D, x.s.data(), 1);
     else
         orc_batch_float_score(&ms, frames.data(), F, D, x.s.data(), 1);
+    x.exact = !kProduct || type == "SIMD-diagonal-maximum" || type == "batch-diagonal-maximum-int";
     return x;
 }
 
@@ -157,20 +195,30 @@ const Mm::AssigningFeatureScorer::AssigningContextScorer* unscaled(const Mm::Fea
 }
 
 void runRecognizer(const Model& m, const std::string& type, u32 B, const std::vector<float>& frames, uint32_t F,
-                   uint32_t segments, const Expected& ex, const std::string& shardDevices = "") {
+                   uint32_t segments, const Expected& ex, bool askBest, const std::string& shardDevices = "") {
     auto           scorer = create(m, type, B, shardDevices);
     const uint32_t M = m.ms->nMixtures(), D = m.ms->dimension();
-    const bool     assigning = type == "SIMD-diagonal-maximum" || type == "diagonal-maximum";
-    uint32_t       t = 0, bad = 0, badBest = 0;
+    const bool     assigning = askBest && (type == "SIMD-diagonal-maximum" || type == "diagonal-maximum");
+    uint32_t       t = 0, bad = 0, badBest = 0, nearTies = 0;
     check(scorer->isBuffered() == (B > 1 || type.rfind("batch", 0) == 0), type + ": isBuffered");
     check(scorer->bufferSize() == (scorer->isBuffered() ? B : 0u), type + ": bufferSize");
     auto feed = [&](const Mm::FeatureScorer::Scorer& s) {  // the search reads score(e); an aligner bestDensity(e)
         check(s->nEmissions() == M, type + ": nEmissions");
         for (uint32_t e = 0; e < M; ++e) {
             const float want = 0.75f * ex.s[static_cast<size_t>(e) * F + t], got = s->score(e);
-            if (std::memcmp(&want, &got, sizeof(float)) != 0)  // bit for bit
+            if (!sameScore(want, got, ex.exact))
                 ++bad;
-            if (assigning && unscaled(s)->bestDensity(e) != ex.b[static_cast<size_t>(e) * F + t])
+            if (!assigning)
+                continue;
+            const uint32_t gotB = unscaled(s)->bestDensity(e), wantB = ex.b[static_cast<size_t>(e) * F + t];
+            if (gotB == wantB)
+                continue;
+            const float* x = &frames[static_cast<size_t>(t) * D];
+            if (!ex.exact && gotB < m.off[e + 1] - m.off[e] &&
+                std::fabs(f64Score(m, x, e, gotB) - f64Score(m, x, e, wantB)) <=
+                        1e-4 * std::max(1.0, std::fabs(f64Score(m, x, e, wantB))))
+                ++nearTies;  // the float contract: either of two densities whose scores agree within 1e-4
+            else
                 ++badBest;
         }
         ++t;
@@ -193,9 +241,11 @@ void runRecognizer(const Model& m, const std::string& type, u32 B, const std::ve
     check(t == F, type + ": every frame fed once");
     check(bad == 0, type + " buffer " + std::to_string(B) + ": " + std::to_string(bad) + " scaled scores differ");
     check(badBest == 0, type + " buffer " + std::to_string(B) + ": " + std::to_string(badBest) + " best densities differ");
-    std::printf("recognizer %-30s buffer-size %5u%s: %u frames x %u emissions, scores %s, best densities %s\n", type.c_str(),
-                B, shardDevices.empty() ? "" : (" density-shard-devices " + shardDevices).c_str(), F, M,
-                bad ? "DIFFER" : "equal", assigning ? (badBest ? "DIFFER" : "equal") : "n/a");
+    std::printf("recognizer %-30s buffer-size %5u%s %-7s: %u frames x %u emissions, scores %s, best densities %s%s\n",
+                type.c_str(), B, shardDevices.empty() ? "" : (" density-shard-devices " + shardDevices).c_str(),
+                askBest ? "aligner" : "search", F, M, bad ? "DIFFER" : (ex.exact ? "equal" : "within 1e-4"),
+                assigning ? (badBest ? "DIFFER" : "equal") : "n/a",
+                nearTies ? (" (" + std::to_string(nearTies) + " near ties)").c_str() : "");
 }
 
 void runScoreDump(const Model& m, const std::string& type, u32 B, const std::vector<float>& frames, uint32_t F,
@@ -226,13 +276,15 @@ void runScoreDump(const Model& m, const std::string& type, u32 B, const std::vec
     for (size_t i = 0; i < dump.size() && dump.size() == 2u * F * M; ++i) {
         const uint32_t f = static_cast<uint32_t>((i / M) % F), e = static_cast<uint32_t>(i % M);
         const float want = -(0.75f * ex.s[static_cast<size_t>(e) * F + f]);
-        if (std::memcmp(&want, &dump[i], sizeof(float)) != 0)
+        if (!sameScore(want, dump[i], ex.exact))
             ++bad;
     }
     check(bad == 0, type + " dump: " + std::to_string(bad) + " values differ");
-    std::printf("score dump %-30s buffer-size %5u: 2 segments x %u frames, %s\n", type.c_str(), B, F, bad ? "DIFFER" : "equal");
+    std::printf("score dump %-30s buffer-size %5u: 2 segments x %u frames, %s\n", type.c_str(), B, F,
+                bad ? "DIFFER" : (ex.exact ? "equal" : "within 1e-4"));
 }
 
+#ifndef HARNESS_PRODUCT
 // a type without assignments asked for bestDensity(): the adapter routes the error to the component's
 // criticalError (Core::Component::criticalError aborts) -- run in a child
 void checkCriticalErrorRouting(const Model& m, const std::vector<float>& frames) {
@@ -266,9 +318,13 @@ void checkCriticalErrorRouting(const Model& m, const std::vector<float>& frames)
     std::printf("criticalError routing: batch type bestDensity() -> %s\n", aborted ? "component criticalError, abort" : "NOT ABORTED");
 }
 
+#endif
+
 }  // namespace
 
+#ifndef HARNESS_PRODUCT
 extern std::vector<int> gStandinShardDevices;  // gmm_standin.cc
+#endif
 
 int main() {
     Mm::registerGpuFeatureScorers(0x500);
@@ -278,32 +334,49 @@ int main() {
           "gpu-SIMD-diagonal-maximum at 0x500");
     check(Mm::Module::instance().featureScorerFactory()->idOf("gpu-batch-diagonal-maximum-int", id) && id == 0x502,
           "gpu-batch-diagonal-maximum-int at 0x502");
-    const uint32_t     D = 39, M = 40, F = 150;
+    // 3 segments of 700 frames: a 512-frame ring fills, wraps and prefetches inside every segment
+    const uint32_t     D = 39, M = 40, F = 2100;
     const Model        model = makeModel(D, M, 7);
     std::vector<float> frames(static_cast<size_t>(F) * D);
     Rng                rng{11};
     for (auto& x : frames)
         x = rng.normal();
+    std::printf("adapter over %s\n", kProduct ? "librasr_gmm.so (HIP)" : "the oracle-backed C-ABI stand-in");
     const char* types[] = {"SIMD-diagonal-maximum", "diagonal-maximum", "batch-diagonal-maximum-int",
                            "batch-diagonal-maximum-float"};
     for (const char* type : types) {
-        const Expected ex = oracleScores(model, type, frames, F);
-        for (u32 B : {1u, 4u, 64u}) {
+        const Expected ex        = oracleScores(model, type, frames, F);
+        const bool     assigning = std::string(type) == "SIMD-diagonal-maximum" || std::string(type) == "diagonal-maximum";
+        for (u32 B : {1u, 4u, 64u, 512u}) {
             if (B == 1 && std::string(type).rfind("batch", 0) == 0)
                 continue;  // the batch types are always buffered
-            runRecognizer(model, type, B, frames, F, 3, ex);
+            runRecognizer(model, type, B, frames, F, 3, ex, false);
+            if (assigning)
+                runRecognizer(model, type, B, frames, F, 3, ex, true);
             runScoreDump(model, type, B, frames, F, ex);
         }
     }
     // "density-shard-devices" reaches gmm_scorer_create_sharded with the configured device list
     {
         const Expected ex = oracleScores(model, "SIMD-diagonal-maximum", frames, F);
+#ifdef HARNESS_PRODUCT
+        // three density parts on device 0 (the copy exchange; the library's one-GPU form of config 4)
+        for (u32 B : {64u, 512u}) {
+            runRecognizer(model, "SIMD-diagonal-maximum", B, frames, F, 3, ex, true, "0,0,0");
+            runRecognizer(model, "SIMD-diagonal-maximum", B, frames, F, 3, ex, false, "0,0,0");
+        }
+        const Expected exi = oracleScores(model, "batch-diagonal-maximum-int", frames, F);
+        runRecognizer(model, "batch-diagonal-maximum-int", 512, frames, F, 3, exi, false, "0,0,0");
+#else
         gStandinShardDevices.clear();
-        runRecognizer(model, "SIMD-diagonal-maximum", 64, frames, F, 3, ex, "0,1,2");
+        runRecognizer(model, "SIMD-diagonal-maximum", 64, frames, F, 3, ex, true, "0,1,2");
         check(gStandinShardDevices == std::vector<int>({0, 1, 2}), "density-shard-devices -> gmm_scorer_create_sharded");
         std::printf("density-shard-devices 0,1,2 -> gmm_scorer_create_sharded over %zu devices\n", gStandinShardDevices.size());
+#endif
     }
+#ifndef HARNESS_PRODUCT
     checkCriticalErrorRouting(model, frames);
+#endif
     std::printf("%s (%d failures)\n", gFailures ? "FAILED" : "PASSED", gFailures);
     return gFailures ? 1 : 0;
 }

@@ -1,5 +1,6 @@
 // TEST DOUBLE: Mm::MixtureSet with the accessors the adapter's conversion reads
 #pragma once
+#include <cmath>
 #include <vector>
 #include <Core/ReferenceCounting.hh>
 #include "Types.hh"
@@ -36,6 +37,7 @@ public:
     DensityIndex nDensities() const { return static_cast<DensityIndex>(d_.size()); }
     DensityIndex densityIndex(DensityIndex j) const { return d_[j]; }
     Weight       logWeight(size_t j) const { return w_[j]; }
+    Weight       weight(size_t j) const { return std::exp(w_[j]); }  // Mixture::weight, src/Mm/Mixture.hh
 
 private:
     std::vector<DensityIndex> d_;

@@ -49,13 +49,36 @@ def test_batch_fast_restatement_refuses_small_dimensions(dim):
 def test_adapter_linked_and_run_in_plugin_harness():
     """integration/rasr/Mm/GpuFeatureScorer.cc linked with the real host classes inside test doubles of RASR's
     plugin machinery (tests/rasr_harness/include/README) over an oracle-backed stand-in of the C-ABI, and driven
-    through FeatureScorerFactory, FeatureScorerScaling, the OfflineRecognizer and FeatureScorerNode call
-    sequences at buffer sizes 1, 4 and 64 (make check-integration-link): every scaled score and best density
-    equals the oracle's, "density-shard-devices" reaches gmm_scorer_create_sharded, and a type without assignments
-    routes bestDensity() to the component's criticalError."""
+    through FeatureScorerFactory, FeatureScorerScaling, the OfflineRecognizer (search and aligner reads) and
+    FeatureScorerNode call sequences at buffer sizes 1, 4, 64 and 512 (make check-integration-link): every scaled
+    score and best density equals the oracle's, "density-shard-devices" reaches gmm_scorer_create_sharded, and a
+    type without assignments routes bestDensity() to the component's criticalError."""
     r = subprocess.run(["make", "-s", "-C", ROOT, "check-integration-link"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "PASSED (0 failures)" in r.stdout
-    assert r.stdout.count("score dump") == 10 and r.stdout.count("recognizer ") == 11 and "DIFFER" not in r.stdout
+    assert r.stdout.count("score dump") == 14 and r.stdout.count("recognizer ") == 23 and "DIFFER" not in r.stdout
     assert "density-shard-devices 0,1,2 -> gmm_scorer_create_sharded over 3 devices" in r.stdout
     assert "component criticalError, abort" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_adapter_over_product_library_on_gpu(gpu):
+    """The same adapter and harness linked against the PRODUCT library librasr_gmm.so (the HIP kernels; the oracle
+    is only the checker), run on the GPU: registerGpuFeatureScorers -> FeatureScorerFactory -> FeatureScorerScaling,
+    the recognizer sequence (search: score(e); aligner: score(e) + bestDensity(e)) and the FeatureScorerNode dump at
+    buffer sizes 1, 4, 64 and 512 (512 and 64: the asynchronous prefetch), and density-shard-devices 0,0,0 (three
+    density parts on one GPU, the copy exchange).  SIMD and batch-int: every scaled score and best density bit for
+    bit; float types within 1e-4 relative, best densities equal except at near ties (both f64 scores within 1e-4)."""
+    exe = os.path.join(ROOT, "build", "tests", "rasr_adapter_harness_gpu")
+    assert os.path.exists(exe), "build it with make (it travels with the tree)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=540)
+    out = r.stdout
+    assert r.returncode == 0, out[-4000:] + r.stderr[-3000:]
+    assert "adapter over librasr_gmm.so (HIP)" in out
+    assert "PASSED (0 failures)" in out and "DIFFER" not in out
+    assert out.count("score dump") == 14 and out.count("recognizer ") == 27
+    assert out.count("density-shard-devices 0,0,0") == 5
+    for t in ("SIMD-diagonal-maximum", "batch-diagonal-maximum-int"):  # the exact types stay exact
+        assert all("within" not in line for line in out.splitlines() if f" {t} " in line)
+    print(out)

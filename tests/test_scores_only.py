@@ -64,6 +64,12 @@ def test_simd_scores_only_bit_exact(gpu, case):
     assert np.array_equal(b2, ref_b)
     keys = ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=f, full_keys=True)
     _same(keys.score_host(frames, want_best=False)[0], ref_s)
+    # without the score-only twin (GMM_FLAG_NO_SCORE_ONLY_TWIN) every call runs the key layout: same scores
+    lone = ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=f, no_score_only_twin=True)
+    _same(lone.score_host(frames, want_best=False)[0], ref_s)
+    s3, b3 = lone.score_host(frames)
+    _same(s3, ref_s)
+    assert np.array_equal(b3, ref_b)
 
 
 def test_simd_scores_only_edge_frames(gpu):
@@ -208,8 +214,13 @@ def test_diagonal_sum_scores_only(gpu, case):
     s, _ = sc.score_host(frames, want_best=False)
     fin = np.isfinite(ref)
     assert np.array_equal(np.isfinite(s), fin)
-    err = np.abs(s.astype(np.float64) - ref)[fin] / np.maximum(1.0, np.abs(ref[fin].astype(np.float64)))
+    # empty mixtures: the non-finite value itself (NaN or the sign of an infinity) must match, exactly
+    assert np.array_equal(s[~fin], ref[~fin], equal_nan=True), f"non-finite {s[~fin][:5]} vs {ref[~fin][:5]}"
+    r64 = ref[fin].astype(np.float64)  # masked before subtracting: no inf - inf
+    err = np.abs(s[fin].astype(np.float64) - r64) / np.maximum(1.0, np.abs(r64))
     assert err.max() <= REL_TOL, f"max rel err {err.max()}"
     sk, _ = sc.score_host(frames)
-    err2 = np.abs(sk.astype(np.float64) - s)[fin] / np.maximum(1.0, np.abs(s[fin].astype(np.float64)))
+    assert np.array_equal(sk[~fin], s[~fin], equal_nan=True)
+    s64 = s[fin].astype(np.float64)
+    err2 = np.abs(sk[fin].astype(np.float64) - s64) / np.maximum(1.0, np.abs(s64))
     assert err2.max() <= 1e-5, f"with vs without best densities {err2.max()}"

@@ -4,8 +4,8 @@ keys, the full table assembled on devices[0].
 
 CPU: the C++ shard plan (gmm_density_shard_plan, rasr_amd/csrc/gmm_shard.cc) equals the Python plan
 (rasr_amd/parallel.py density_shards) on ragged, empty-mixture and tiny models; argument checks.
-GPU: N parts on ONE GPU with the copy exchange (RCCL refuses two ranks on one device; the RCCL exchange runs the
-same plan, packing and unpacking with an all-reduce in place of the peer copies + minimum kernel) against the
+GPU: N parts on ONE GPU with the copy exchange (AUTO's choice when all parts share a GPU; the RCCL exchange on one
+GPU, a one-rank all-reduce after an on-device fold, is tests/test_rccl_exchange.py) against the
 unsharded scorer -- bit for bit for the quantized types (scores and best densities), within the float contract
 for diagonal-maximum (checked against the oracle as tests/test_density_sharded.py does) -- through
 gmm_score_host, gmm_score_host_ring (frame-major, keep-best + fetch) and gmm_score_device; N = 1 is the
@@ -184,8 +184,9 @@ def test_sharded_refusals(gpu):
     for kind in ("diagonal-sum", "preselection-batch-int", "preselection-batch-float"):
         with pytest.raises(_capi.GmmError):
             ra.Scorer(ms, kind, max_frames=16, devices=[0, 0])
-    with pytest.raises(_capi.GmmError, match="distinct devices"):
-        ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=16, devices=[0, 0], exchange="rccl")
+    # parts sharing a GPU fold their keys on it before the all-reduce: RCCL over [0, 0] is a one-rank communicator
+    assert ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=16, devices=[0, 0], exchange="rccl").shard_info() == \
+        (2, "rccl")
     with pytest.raises(_capi.GmmError):
         ra.Scorer(ms, "SIMD-diagonal-maximum", max_frames=16, devices=[0, 0], mixture_range=(0, 10))
     with pytest.raises(_capi.GmmError):
