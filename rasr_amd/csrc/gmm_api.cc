@@ -153,7 +153,7 @@ struct gmm_scorer {
     DensityClustering       clustering;
     void*                   dClusterMeans = nullptr;
     uint32_t*               dSelT         = nullptr;  // [nFramesPad/64][clusters][16]
-    uint16_t*               dTileClu      = nullptr;  // [tiles + pad][16] cluster * 64
+    void*                   dTileClu      = nullptr;  // [tiles + pad][16]: u16 cluster * 64 (float), u32 cluster * 16 (int)
     uint32_t                lastFrames    = 0;
     // quantized scalars
     uint32_t idxBits = 1, paddedDimension = 0;
@@ -569,16 +569,36 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
         return fail(GMM_ERR_INVALID_ARGUMENT, err);
     const DensityClustering& dc = s->clustering;
     const uint32_t           T  = static_cast<uint32_t>(rowEntry.size() / kTileRows);
-    std::vector<uint16_t>    clu(static_cast<size_t>(T + kTilePad) * kTileRows, 0);
-    for (uint32_t t = 0; t < T; ++t)
-        for (uint32_t r = 0; r < kTileRows; ++r) {
-            uint32_t e = rowEntry[static_cast<size_t>(t) * kTileRows + r];
-            if (e == UINT32_MAX && fill)
-                e = (*fill)[t];
-            const uint32_t c = e == UINT32_MAX ? 0u : dc.clusterOfEntry[e];
-            clu[static_cast<size_t>(t) * kTileRows + r] = static_cast<uint16_t>(c * 64u);
-        }
-    int rc = upload(&s->dTileClu, clu);
+    // per tile row: the byte offset of its cluster in a wave's mask table -- the float kernel's word table
+    // (u16, 64 B per cluster), the quantized kernel's byte table (u32, 16 B per cluster, whose entry nClusters is
+    // "never selected": the padding rows' cluster, so a frame that selected none of a mixture's rows keeps all
+    // ones; one u32 per row so a lane group's 4 rows are one aligned 16-byte word)
+    const auto clusterOf = [&](uint32_t t, uint32_t r) -> uint32_t {
+        uint32_t e = rowEntry[static_cast<size_t>(t) * kTileRows + r];
+        if (e == UINT32_MAX && fill)
+            e = (*fill)[t];
+        return e == UINT32_MAX ? (s->quantized ? dc.nClusters : 0u) : dc.clusterOfEntry[e];
+    };
+    int rc;
+    if (s->quantized) {
+        const uint32_t        per = 16u * kI8PreselEntryBytes;
+        std::vector<uint32_t> clu(static_cast<size_t>(T + kTilePad) * kTileRows, dc.nClusters * per);
+        for (uint32_t t = 0; t < T; ++t)
+            for (uint32_t r = 0; r < kTileRows; ++r)
+                clu[static_cast<size_t>(t) * kTileRows + r] = clusterOf(t, r) * per;
+        uint32_t* d = nullptr;
+        rc          = upload(&d, clu);
+        s->dTileClu = d;
+    }
+    else {
+        std::vector<uint16_t> clu(static_cast<size_t>(T + kTilePad) * kTileRows, 0);
+        for (uint32_t t = 0; t < T; ++t)
+            for (uint32_t r = 0; r < kTileRows; ++r)
+                clu[static_cast<size_t>(t) * kTileRows + r] = static_cast<uint16_t>(clusterOf(t, r) * 64u);
+        uint16_t* d = nullptr;
+        rc          = upload(&d, clu);
+        s->dTileClu = d;
+    }
     if (rc != GMM_OK)
         return rc;
     if (s->quantized)
@@ -1143,8 +1163,9 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
     if (quantized) {
         PreparedQuantized p;
         // batch types have no best densities: the score-only class layout where it applies
+        // (preselection-batch-int included: the kernel masks the class layout's candidates)
         const bool        scoreOnlyLayout =
-                classLayout || (!presel && flavor == Flavor::BatchInt && !(cfg.flags & GMM_FLAG_FULL_KEYS));
+                classLayout || (flavor == Flavor::BatchInt && !(cfg.flags & GMM_FLAG_FULL_KEYS));
         std::string       err = prepareQuantized(*ms, flavor, shard, p, scoreOnlyLayout);
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);

@@ -60,7 +60,7 @@ struct I8Args {
     double          halfInvS2;    // 0.5 * RN64(1 / s2) for the SIMD finalize, 0 = always divide (gmm_kernels_i8.hip)
     // preselection-batch-int (gmm_kernels_presel.hip): per-(frame, cluster) mask, per-row cluster offsets
     const uint32_t* selT;         // [nFramesPad/64][nClusters][16] u32, byte (frame%64)/16 = 0xff: deselected
-    const void*     tileClu;      // u16 [T+pad][16]: cluster * 64 (byte offset into a wave's mask table)
+    const void*     tileClu;      // u32 [T+pad][16]: cluster * 16 * kI8PreselEntryBytes (byte offset into a wave's table)
     uint32_t        nClusters;
     int             presel;
     // score-only class layout (batch types, gmm_prepare.hh PreparedQuantized::scoreOnly): tileP is the
@@ -175,8 +175,14 @@ hipError_t launchScoreDirect(const DirectArgs& a, hipStream_t stream);
 uint32_t   directBlocks(uint32_t D, bool batch);  // 4-dimension blocks of the row layout, 0 = unsupported
 // quantized LDS kernel: the never-winning stand-in tile after the segment ring (operands, row constants,
 // PRESEL cluster offsets)
-constexpr uint32_t kI8DummyTileBytes(int ks, bool presel) { return static_cast<uint32_t>(ks) * 1024u + 64u + (presel ? 32u : 0u); }
-constexpr uint32_t kI8PreselNF           = 4;  // preselection-batch-int: 64 frames per wave (one mask word)
+constexpr uint32_t kI8DummyTileBytes(int ks, bool presel) { return static_cast<uint32_t>(ks) * 1024u + 64u + (presel ? 64u : 0u); }
+#ifndef GMM_I8_PRESEL_NF
+#define GMM_I8_PRESEL_NF 8
+#endif
+// preselection-batch-int: frames per wave / 16 (8: two 64-frame mask words per wave; 4 kept for A/B)
+constexpr uint32_t kI8PreselNF           = GMM_I8_PRESEL_NF;
+// bytes of a mask table entry (gmm_kernels_i8.hip): a row's cluster offset is cluster * 16 * this
+constexpr uint32_t kI8PreselEntryBytes   = kI8PreselNF == 8 ? 2 : 1;
 constexpr uint32_t kI8PreselFramesPerBlock = kWavesPerBlock * kI8PreselNF * 16;
 
 // density-sharded exchange (gmm_kernels_shard.hip): (score, density) <-> order-preserving int64 keys

@@ -27,6 +27,8 @@
 // uses __fmul_rn / __fadd_rn so it can never be contracted into an FMA.
 //
 // This file: the quantized kernels (built with -mllvm -amdgpu-mfma-vgpr-form, see Makefile).
+#include <type_traits>
+
 #include "gmm_device.hh"
 
 #ifndef GMM_I8_SLOTS
@@ -336,10 +338,15 @@ extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 // mixTileOff / scores / best are separate __restrict__ parameters so the mixture boundaries are read
 // with scalar loads (a vector load would need an s_waitcnt vmcnt(0) that drains the LDS-DMA queue).
 //
-// PRESEL (preselection-batch-int, NF = 4: one 64-frame mask word per wave): keys are biased by 2^31
+// PRESEL (preselection-batch-int, NF = kI8PreselNF: 8, a wave's 128 frames are two 64-frame mask words; 4 kept
+// for A/B): keys are biased by 2^31
 // (the packed row constant XOR 2^31) and compared unsigned, so OR-ing the sign-extended mask byte of a
 // (frame, density cluster) that the frame did not select makes the all-ones key, which never wins; the
-// segment carries each tile's 16 row offsets into the wave's mask table (gmm_kernels_presel.hip).
+// segment carries each tile's 16 row byte offsets into the wave's mask table (gmm_kernels_presel.hip).  The
+// table has one entry past the clusters, "never selected", for padding rows and the stand-in tile.
+// PRESEL with SCORE_ONLY (the default for preselection-batch-int, a batch type without best densities): the
+// class layout below with the biased h as the MFMA's C input, so a class candidate is the accumulator u = v + 2^31
+// and the mask is one v_or per candidate (no pack); a mixed candidate is 2 u + (p | 2^31) = 2 v + p + 2^31.
 #ifndef GMM_I8_WAVES
 #define GMM_I8_WAVES 4  // scoreI8Seg, one K step: waves per SIMD the register allocation must allow (0 = free)
 #endif
@@ -357,14 +364,19 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                                                    float* __restrict__ scores, uint32_t* __restrict__ bestOut,
                                                    const uint32_t* __restrict__ mixOddMask = nullptr) {
     static_assert(NF == 4 || NF == 8, "NF");
-    static_assert(!PRESEL || NF == 4, "preselection masks are 64-frame words");
-    static_assert(!SCORE_ONLY || (!PRESEL && KS == 1), "score-only layout: one K step, no preselection");
+    static_assert(!PRESEL || NF == 4 || NF == 8, "preselection masks: one or two 64-frame words per wave");
+    // PRESEL mask table entries: NF 4 a byte (4 deselection bits x 4: the byte offset of a u32 in maskLut), NF 8 a
+    // u16 (8 bits x 8: the byte offset of a u64 in maskLut)
+    constexpr uint32_t kEntryBytes = NF == 8 ? 2u : 1u;
+    typedef typename std::conditional<NF == 8, uint64_t, uint32_t>::type LutW;  // a maskLut entry
+    typedef uint2 MaskW;  // a row's mask bytes as registers: x blocks 0-3, y blocks 4-7 (NF 8)
+    static_assert(!SCORE_ONLY || KS == 1, "score-only layout: one K step");
     constexpr int      kSegTiles = SEG;
     constexpr int      NPL       = NF / 4;
     constexpr uint32_t kTileA    = KS * 1024;                   // operand bytes per tile
     constexpr uint32_t kSegA     = kSegTiles * kTileA;
     constexpr uint32_t kSegP     = kSegA + kSegTiles * 64;      // + packed row constants
-    constexpr uint32_t kSegBytes = kSegP + (PRESEL ? kSegTiles * 32 : 0);  // + row cluster offsets (u16)
+    constexpr uint32_t kSegBytes = kSegP + (PRESEL ? kSegTiles * 64 : 0);  // + row cluster offsets (u32)
     constexpr int      kPieces   = kSegTiles * KS / 4;          // 1 KiB pieces per wave per segment
     constexpr int      kIssued   = kPieces + 1 + (PRESEL ? 1 : 0);  // vector memory ops per wave per segment
     static_assert(kSegTiles * KS % 4 == 0, "segment pieces must split evenly over 4 waves");
@@ -373,9 +385,20 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     // step: one loop body, whose running minima stay in their registers (a second, single-tile body made
     // the compiler copy all NF*4 minima back at every step that did not end a mixture)
     constexpr uint32_t kDummyBytes = kI8DummyTileBytes(KS, PRESEL);
-    // one __shared__ array only (a second one can make hipcc drain vmcnt before LDS reads)
-    __shared__ __attribute__((aligned(16))) int8_t ldsStatic[PRESEL ? 16 : 2 * kSegBytes + kDummyBytes];
-    int8_t* const lds = PRESEL ? i8DynLds : ldsStatic;
+    // one __shared__ array per instantiation: PRESEL the dynamic one only (its size depends on the cluster count)
+    // PRESEL: the 16-entry mask LUT is a static array (its address folds into the ds_read offset; the dynamic
+    // array's base is a relocation the compiler adds per read), ring and tables the dynamic one
+    int8_t* lds;
+    LutW*   maskLut = nullptr;
+    if constexpr (PRESEL) {
+        __shared__ LutW lutStatic[NF == 8 ? 256 : 16];
+        lds     = i8DynLds;
+        maskLut = lutStatic;
+    }
+    else {
+        __shared__ __attribute__((aligned(16))) int8_t ldsStatic[2 * kSegBytes + kDummyBytes];
+        lds = ldsStatic;
+    }
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -406,19 +429,23 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         if (lane < kSegTiles)  // kSegTiles tiles x 64 B of row constants: 16 kSegTiles B per wave
             __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * (kSegTiles * 16) + lane * 16,
                                              base + kSegA + wave * (kSegTiles * 16), 16, 0, 0);
-        if constexpr (PRESEL) {  // kSegTiles tiles x 32 B of row cluster offsets: 8 kSegTiles B per wave
-            if (lane < kSegTiles / 2)
-                __builtin_amdgcn_global_load_lds(gClu + static_cast<size_t>(t0) * 32 + wave * (kSegTiles * 8) + lane * 16,
-                                                 base + kSegP + wave * (kSegTiles * 8), 16, 0, 0);
+        if constexpr (PRESEL) {  // kSegTiles tiles x 64 B of row cluster offsets: 16 kSegTiles B per wave
+            if (lane < kSegTiles)
+                __builtin_amdgcn_global_load_lds(gClu + static_cast<size_t>(t0) * 64 + wave * (kSegTiles * 16) + lane * 16,
+                                                 base + kSegP + wave * (kSegTiles * 16), 16, 0, 0);
         }
     };
     {
         int8_t* const dummy = lds + 2 * kSegBytes;
-        // non-PRESEL rows compare signed (INT_MAX never wins), PRESEL rows unsigned (biased: all ones);
+        // non-PRESEL rows compare signed (INT_MAX never wins), PRESEL rows unsigned (biased: all ones, and their
+        // rows sit in the never-selected cluster, so every kind of step masks them to all ones);
         // SCORE_ONLY: the class layout's padding value (2 v + 1 of a mixed step stays inside int32)
-        const uint32_t never = PRESEL ? 0xffffffffu : (SCORE_ONLY ? 0x30000000u : 0x7fffffffu);
+        const uint32_t never    = PRESEL ? 0xffffffffu : (SCORE_ONLY ? 0x30000000u : 0x7fffffffu);
+        const uint32_t neverClu = PRESEL ? a.nClusters * 16u * kEntryBytes : 0u;  // u32 row offsets
         for (uint32_t i = threadIdx.x; i < kDummyBytes / 4; i += 256u)
-            reinterpret_cast<uint32_t*>(dummy)[i] = (i >= kTileA / 4 && i < kTileA / 4 + 16) ? never : 0u;
+            reinterpret_cast<uint32_t*>(dummy)[i] = (i >= kTileA / 4 && i < kTileA / 4 + 16)
+                                                            ? never
+                                                            : (i >= kTileA / 4 + 16 ? neverClu : 0u);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before use by the first segment's barrier
     }
     if (nSeg > 0)
@@ -440,47 +467,74 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     for (int i = 0; i < NPL; ++i)
         ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
 
-    // preselection: this wave's 64-frame mask table [cluster][16] after the segment ring
+    // preselection: this wave's mask table [cluster][16] after the segment ring
     uint32_t laneSel = 0;  // byte offset of (wave table, column t = lane & 15)
-    // compressed: one byte per (cluster, t) whose bit cb says "frame 16 cb + t did not select the cluster"
-    // (4 KiB per wave instead of 16: 5 workgroups per CU instead of 2), expanded back to the 4-byte mask
-    // word by a 16-entry table after the ring
-    const uint32_t lutOff = 2 * kSegBytes + kDummyBytes;
+    // compressed: per (cluster, t) the bits "frame 16 cb + t did not select the cluster" (bit cb), stored as the byte
+    // offset of the entry of maskLut that expands them to one 0x00 / 0xff mask byte per column block (NF 4: 4 KiB
+    // per wave instead of 16, 5 workgroups per CU instead of 2)
+    const uint32_t tabBase = 2 * kSegBytes + kDummyBytes;
     if constexpr (PRESEL) {
-        const uint32_t words = a.nClusters * 16u;
-        if (threadIdx.x < 16u) {
-            const uint32_t n = threadIdx.x;
-            reinterpret_cast<uint32_t*>(lds + lutOff)[n] =
-                    ((n & 1u) ? 0xffu : 0u) | ((n & 2u) ? 0xff00u : 0u) | ((n & 4u) ? 0xff0000u : 0u) | ((n & 8u) ? 0xff000000u : 0u);
-        }
-        const uint32_t tabOff = lutOff + 64u + static_cast<uint32_t>(wave) * words;
-        const i32x4*   src    = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
-        uint32_t*      dst    = reinterpret_cast<uint32_t*>(lds + tabOff);
-        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u) {
-            const i32x4 w = src[i];
-            uint32_t    packed = 0;
+        const uint32_t words = a.nClusters * 16u;  // u32 words of a 64-frame selection block (and table entries)
+        for (uint32_t n = threadIdx.x; n < (NF == 8 ? 256u : 16u); n += 256u) {
+            LutW v = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)  // bit 0 of each byte (0x00 / 0xff) -> bits 0..3 of the top byte
-                packed |= (((static_cast<uint32_t>(w[j]) & 0x01010101u) * 0x01020408u) >> 24) << (8 * j);
-            dst[i] = packed;
+            for (int cb = 0; cb < NF; ++cb)
+                v |= ((n >> cb) & 1u) ? LutW(0xff) << (8 * cb) : LutW(0);
+            maskLut[n] = v;
         }
-        laneSel = tabOff + (static_cast<uint32_t>(lane) & 15u);
+        const uint32_t tabOff = tabBase + static_cast<uint32_t>(wave) * (words + 16u) * kEntryBytes;
+        // the selection words of this wave's frames: one 64-frame block (NF 4) or two (NF 8); bit 0 of byte q
+        // (0x00 / 0xff) of a word says frame 16 q + t of the block did not select the cluster
+        const i32x4* src0 = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
+        const i32x4* src1 = src0 + words / 4u;
+        const auto   nib  = [](uint32_t w) { return ((w & 0x01010101u) * 0x01020408u) >> 24 & 0xfu; };  // bit q = byte q
+        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u) {
+            const i32x4 w0 = src0[i];
+            if constexpr (NF == 8) {
+                const i32x4 w1 = src1[i];
+                uint32_t    e[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)  // entry: 8 * (bits of block 0 | bits of block 1 << 4)
+                    e[j] = (nib(static_cast<uint32_t>(w0[j])) | nib(static_cast<uint32_t>(w1[j])) << 4) * 8u;
+                reinterpret_cast<uint2*>(lds + tabOff)[i] = uint2{e[0] | e[1] << 16, e[2] | e[3] << 16};
+            }
+            else {
+                uint32_t packed = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)  // entry: 4 * the 4 bits
+                    packed |= (nib(static_cast<uint32_t>(w0[j])) * 4u) << (8 * j);
+                reinterpret_cast<uint32_t*>(lds + tabOff)[i] = packed;
+            }
+        }
+        // the never-selected cluster: every frame deselected, in all 16 columns
+        if (lane < 4)
+            reinterpret_cast<uint32_t*>(lds + tabOff + words * kEntryBytes)[lane] = NF == 8 ? 0x07f807f8u : 0x3c3c3c3cu;
+        if (NF == 8 && lane >= 4 && lane < 8)
+            reinterpret_cast<uint32_t*>(lds + tabOff + words * kEntryBytes)[lane] = 0x07f807f8u;
+        laneSel = tabOff + (static_cast<uint32_t>(lane) & 15u) * kEntryBytes;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the table before the first segment's barrier
     }
     // a tile's row constants (the host biases them by 2^31 for PRESEL) and mask words of this lane's 4 rows,
-    // from the tile's 64-byte row-constant block pRow and 32-byte cluster-offset block cRow
-    const auto tileRows = [&](const int8_t* pRow, const int8_t* cRow, i32x4& P, uint32_t(&T)[4]) {
+    // from the tile's 64-byte row-constant block pRow and 64-byte cluster-offset block cRow
+    const auto tileRows = [&](const int8_t* pRow, const int8_t* cRow, i32x4& P, MaskW(&T)[4]) {
         P = *reinterpret_cast<const i32x4*>(pRow + g * 16);
         (void)cRow;
         if constexpr (PRESEL) {
-            const uint2 cw = *reinterpret_cast<const uint2*>(cRow + g * 8);
+            // the lane group's 4 row offsets (u32 cluster * 16 * entry bytes: byte offsets into the wave's table) as
+            // one aligned 16-byte read (a 64-bit read of the DMA-filled ring made the waitcnt pass drain the DMA
+            // queue, s_waitcnt vmcnt(0), at every pair step); table entries are LUT byte offsets
+            const i32x4   c4 = *reinterpret_cast<const i32x4*>(cRow + g * 16);
             const int8_t* tb = lds + laneSel;
-            // row offsets are cluster * 64 (the float kernel's word table); the byte table has 16 B per cluster
-            const uint32_t* lut = reinterpret_cast<const uint32_t*>(lds + lutOff);
-            T[0] = lut[*reinterpret_cast<const uint8_t*>(tb + ((cw.x & 0xffffu) >> 2))];
-            T[1] = lut[*reinterpret_cast<const uint8_t*>(tb + (cw.x >> 18))];
-            T[2] = lut[*reinterpret_cast<const uint8_t*>(tb + ((cw.y & 0xffffu) >> 2))];
-            T[3] = lut[*reinterpret_cast<const uint8_t*>(tb + (cw.y >> 18))];
+            const int8_t* lu = reinterpret_cast<const int8_t*>(maskLut);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t e = NF == 8 ? *reinterpret_cast<const uint16_t*>(tb + c4[j])
+                                           : *reinterpret_cast<const uint8_t*>(tb + c4[j]);
+                if constexpr (NF == 8)
+                    T[j] = *reinterpret_cast<const uint2*>(lu + e);
+                else
+                    T[j] = uint2{*reinterpret_cast<const uint32_t*>(lu + e), 0u};
+            }
         }
     };
 
@@ -488,11 +542,19 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     const auto     pack = [&](int acc, int p) {
         return static_cast<int>((static_cast<uint32_t>(acc) << sh) + static_cast<uint32_t>(p));
     };
+    // PRESEL: x OR the sign-extended mask byte of column block cb (0xff: the frame did not select the row's
+    // cluster), one v_or_b32_sdwa
+    const auto maskOr = [](int x, MaskW T, int cb) -> int {
+        // the 32-bit half holding block cb's byte (NF 8: the high half for blocks 4-7), then its byte
+        const uint32_t h = (NF == 8 && cb >= 4) ? T.y : T.x;
+        return static_cast<int>(static_cast<uint32_t>(x) |
+                                static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(h >> (8 * (cb & 3))))));
+    };
+    (void)maskOr;
     // candidate key: the packed value; PRESEL: biased, OR the mask byte of column block cb
-    const auto cand = [&](int acc, int p, uint32_t T, int cb) -> int {
+    const auto cand = [&](int acc, int p, MaskW T, int cb) -> int {
         if constexpr (PRESEL)
-            return static_cast<int>(static_cast<uint32_t>(pack(acc, p)) |
-                                    static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(T >> (8 * cb)))));
+            return maskOr(pack(acc, p), T, cb);
         else
             return pack(acc, p);
     };
@@ -519,13 +581,16 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 best[cb][r] = PRESEL ? -1 : (SCORE_ONLY ? 0x3fffffff : INT_MAX);
     };
     // SCORE_ONLY: the class tiles' minima of mixture mm as 2 v + p_g (this lane group's parity there)
+    // PRESEL: biased, u = v + 2^31 -> 2 v + p + 2^31 = 2 u + (p | 2^31), all ones (nothing selected) kept
     const auto toMixed = [&](uint32_t mm) {
-        const uint32_t p = (mixOddMask[mm] >> g) & 1u;
+        const uint32_t p = ((mixOddMask[mm] >> g) & 1u) | (PRESEL ? 0x80000000u : 0u);
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
 #pragma unroll
-            for (int r = 0; r < kSlots; ++r)
-                best[cb][r] = static_cast<int>((static_cast<uint32_t>(best[cb][r]) << 1) + p);
+            for (int r = 0; r < kSlots; ++r) {
+                const uint32_t u = static_cast<uint32_t>(best[cb][r]);
+                best[cb][r]      = static_cast<int>((PRESEL && u == 0xffffffffu) ? u : (u << 1) + p);
+            }
     };
     uint32_t m    = m0;
     uint32_t tEnd = mixTileOff[m0 + 1];
@@ -539,7 +604,17 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 // a mixture without mixed tiles still holds its class minima v: 2 v + p_g (uniform test)
                 if (tCls >= tEnd)
                     toMixed(mm);
-                emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, 0, ssOut);
+                if constexpr (PRESEL) {  // unbiased: 2 v + p, INT_MAX where the frame selected none of its rows
+                    int unb[NF][kSlots];
+#pragma unroll
+                    for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+                        for (int r = 0; r < kSlots; ++r)
+                            unb[cb][r] = static_cast<int>(static_cast<uint32_t>(best[cb][r]) ^ 0x80000000u);
+                    emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, unb, mm, frame0, lane, g, 0, ssOut);
+                }
+                else
+                    emitMixtureI8<NF, kMaybeNone, kSlots>(a, scores, bestOut, best, mm, frame0, lane, g, 0, ssOut);
             }
             else {
                 int none[NF][1];  // a mixture without tiles: Core::Type<int>::max
@@ -605,16 +680,16 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             const int8_t* const a1    = two ? a0 + kTileA : dummy;
             const int8_t* const p0    = base + kSegA + lt * 64;
             const int8_t* const p1    = two ? p0 + 64 : dummy + kTileA;
-            const int8_t* const c0    = base + kSegP + lt * 32;
-            const int8_t* const c1    = two ? c0 + 32 : dummy + kTileA + 64;
+            const int8_t* const c0    = base + kSegP + lt * 64;
+            const int8_t* const c1    = two ? c0 + 64 : dummy + kTileA + 64;
             i32x4               A0[KS], A1[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 A0[ks] = *reinterpret_cast<const i32x4*>(a0 + ks * 1024 + lane * 16);
                 A1[ks] = *reinterpret_cast<const i32x4*>(a1 + ks * 1024 + lane * 16);
             }
-            i32x4    P0, P1;
-            uint32_t T0w[4] = {}, T1w[4] = {};
+            i32x4 P0, P1;
+            MaskW T0w[4] = {}, T1w[4] = {};
             tileRows(p0, c0, P0, T0w);
             tileRows(p1, c1, P1, T1w);
             i32x4      accA[NF], accB[NF];
@@ -643,6 +718,10 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                 for (int r = 0; r < 4; ++r) {
                     asm("v_lshrrev_b32 %0, 31, %1" : "=v"(pA[r]) : "v"(thr - r));
                     asm("v_lshrrev_b32 %0, 31, %1" : "=v"(pB[r]) : "v"(thr - 16 - r));
+                    if constexpr (PRESEL) {  // the bias of the unsigned comparison: p | 2^31
+                        pA[r] |= static_cast<int>(0x80000000u);
+                        pB[r] |= static_cast<int>(0x80000000u);
+                    }
                 }
             };
             const auto epilogueMixed = [&](int cb) {
@@ -651,6 +730,11 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
                     const int ua = static_cast<int>((static_cast<uint32_t>(accA[cb][r]) << 1) + static_cast<uint32_t>(pA[r]));
                     const int ub = static_cast<int>((static_cast<uint32_t>(accB[cb][r]) << 1) + static_cast<uint32_t>(pB[r]));
                     int&      bs = best[cb][r % kSlots];
+                    if constexpr (PRESEL) {  // masked: all ones; biased keys compare unsigned
+                        const int ma = maskOr(ua, T0w[r], cb), mb = maskOr(ub, T1w[r], cb);
+                        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ma), "v"(mb));
+                        continue;
+                    }
                     bs           = min(bs, min(ua, ub));
                     asm volatile("" : "+v"(bs));
                 }
@@ -658,6 +742,13 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             const auto epilogue = [&](int cb) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
+                    if constexpr (kKind == 1 && PRESEL) {
+                        // the accumulators (biased v) OR the mask: compiler-visible reads (hazard wait states)
+                        int&      bs = best[cb][r % kSlots];
+                        const int ma = maskOr(accA[cb][r], T0w[r], cb), mb = maskOr(accB[cb][r], T1w[r], cb);
+                        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(bs) : "v"(bs), "v"(ma), "v"(mb));
+                        continue;
+                    }
                     if constexpr (kKind == 1) {
                         // a compiler-visible min (not inline asm): the accumulators are read soon after their
                         // MFMAs, and only compiler-visible reads get the hazard wait states.  The empty asm keeps
@@ -784,10 +875,20 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
     if constexpr (!MULTI) {
         if (a.presel) {  // preselection-batch-int: NF 4, 4-tile segments (ring + 4 mask tables < 80 KiB)
             constexpr int      kSeg  = 4;
-            constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 32)) + kI8DummyTileBytes(KS, true);
-            const uint32_t     lds   = kRing + 64u + 4u * a.nClusters * 16u;
-            (void)allowDynamicLds(reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>),
-                                  static_cast<int>(kRing + 4u * 256u * 64u));
+            constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 64)) + kI8DummyTileBytes(KS, true);
+            // after the ring, per wave the table of the clusters and the never-selected entry
+            const uint32_t     lds   = kRing + 4u * (a.nClusters + 1u) * 16u * kI8PreselEntryBytes;
+            constexpr int      kMax  = static_cast<int>(kRing + 4u * 257u * 16u * kI8PreselEntryBytes);
+            if constexpr (KS == 1) {
+                if (a.scoreOnly) {  // the class layout (the default)
+                    (void)allowDynamicLds(
+                            reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, 1, true, kSeg, true>), kMax);
+                    hipLaunchKernelGGL((dev::scoreI8Seg<kI8PreselNF, 1, true, kSeg, true>), dim3(grid), dim3(256), lds,
+                                       s, a, a.mixTileOff, a.scores, nullptr, a.mixOddMask);
+                    return;
+                }
+            }
+            (void)allowDynamicLds(reinterpret_cast<const void*>(&dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>), kMax);
             hipLaunchKernelGGL((dev::scoreI8Seg<kI8PreselNF, KS, true, kSeg>), dim3(grid), dim3(256), lds, s, a,
                                a.mixTileOff, a.scores, a.best, nullptr);
             return;
@@ -814,7 +915,7 @@ hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStr
         return hipSuccess;
     if (a.presel && (multiCov || !GMM_I8_LDS || a.nClusters == 0 || a.nClusters > 256 || !a.selT || !a.tileClu))
         return hipErrorInvalidValue;
-    if (a.scoreOnly && (multiCov || kSteps != 1 || !GMM_I8_LDS || a.presel || !a.mixOddMask))
+    if (a.scoreOnly && (multiCov || kSteps != 1 || !GMM_I8_LDS || !a.mixOddMask))
         return hipErrorInvalidValue;
     if (kSteps == 1)
         multiCov ? launchI8T<kI8NF, 1, true>(a, grid, stream) : launchI8T<kI8NF, 1, false>(a, grid, stream);

@@ -42,6 +42,12 @@
 #ifndef GMM_SPLIT_IL
 #define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
 #endif
+#ifndef GMM_SPLIT_TAG_EMIT
+#define GMM_SPLIT_TAG_EMIT 0  // 1: a tile's keys carry (tile << 2) only; the slot r is OR-ed in at the mixture's end
+#endif
+#ifndef GMM_SPLIT_EMIT_FLAT
+#define GMM_SPLIT_EMIT_FLAT 0  // 1: the emit's finalize without the exec-mask branch around the no-candidate case
+#endif
 
 namespace rasr_gmm {
 namespace dev {
@@ -162,8 +168,12 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
                                                  float noneScore, float halfScale) {
     uint32_t k[4];
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-        k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
+    for (int cb = 0; cb < 4; ++cb) {
+        if (GMM_SPLIT_TAG_EMIT && kmask)  // slot r's keys carry tile << 2 only: r joins here (all ones stay)
+            k[cb] = min(umin3(best[cb][0], best[cb][1] | 1u, best[cb][2] | 2u), best[cb][3] | 3u);
+        else
+            k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
+    }
     // groups {g&1, g&1|2} of blocks (0,2) and (1,3): lanes < 32 keep blocks 0, 1, lanes >= 32 blocks 2, 3
     uint32_t w[2], wg[2];
 #pragma unroll
@@ -183,7 +193,9 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
     // midpoint of the masked bits: within 2^-(24 - keyBits) of the minimum's value
     const float kv    = __uint_as_float((key & ~kmask) | ((kmask + 1u) >> 1));
     const bool  none  = !(kv < 1e37f);  // no finite candidate (empty mixture, non-finite frame)
-    const float total = __fsub_rn(ldexpf(kv, eOut), a.offsetK0);
+    float       total = __fsub_rn(ldexpf(kv, eOut), a.offsetK0);
+    if (GMM_SPLIT_EMIT_FLAT)
+        asm volatile("" : "+v"(total));  // computed for every lane: the select below stays a v_cndmask
     // diagonal-maximum: 0.5 total; batch-float keeps an overflowed total (BatchFeatureScorer.cc:468)
     const float score = none ? noneScore
                              : __fmul_rn(a.outScale, (a.flavor == 3 && !(total < 3.40282347e+38f)) ? total : 0.5f * total);
@@ -329,8 +341,9 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         uint32_t tagA[4], tagB[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            tagA[r] = (tl << 2) | r;
-            tagB[r] = ((tl + 1u) << 2) | r;
+            const uint32_t rr = GMM_SPLIT_TAG_EMIT ? 0u : static_cast<uint32_t>(r);
+            tagA[r] = (tl << 2) | rr;
+            tagB[r] = ((tl + 1u) << 2) | rr;
             asm("" : "+s"(tagA[r]), "+s"(tagB[r]));
         }
 #pragma unroll

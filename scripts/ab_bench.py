@@ -3,9 +3,10 @@
 
 Each variant runs in its own subprocess (RASR_GMM_LIB=<so>); rounds are interleaved
 (v1 v2 ... v1 v2 ...) and the median / min kernel time per variant is reported.
-usage: ab_bench.py --mode fp32|simd|sum|bint|simds --rounds 3 lib1.so lib2.so[:split16|:split32|:fullkeys] ...
+usage: ab_bench.py --mode fp32|simd|sum|bint|simds|fp32s|pint|pfloat --rounds 3 lib1.so lib2.so[:split16|:split32|:fullkeys] ...
 (":split16" / ":split32" run that library with GMM_FLAG_SPLIT_TILE16 / _TILE32, ":fullkeys" with GMM_FLAG_FULL_KEYS;
-bint = batch-diagonal-maximum-int, scores only; simds = SIMD-diagonal-maximum without best densities)
+bint = batch-diagonal-maximum-int, scores only; simds = SIMD-diagonal-maximum without best densities; fp32s =
+diagonal-maximum without best densities; pint / pfloat = preselection-batch-int / -float)
 """
 import argparse
 import json
@@ -22,7 +23,8 @@ sys.path.insert(0, os.environ["ROOT"])
 import torch, rasr_amd as ra
 mode = os.environ["MODE"]; F = int(os.environ["FRAMES"])
 kind = {"fp32": "diagonal-maximum", "simd": "SIMD-diagonal-maximum", "sum": "diagonal-sum",
-        "bint": "batch-diagonal-maximum-int", "simds": "SIMD-diagonal-maximum"}[mode]
+        "bint": "batch-diagonal-maximum-int", "simds": "SIMD-diagonal-maximum", "fp32s": "diagonal-maximum",
+        "pint": "preselection-batch-int", "pfloat": "preselection-batch-float"}[mode]
 D = int(os.environ.get("DIM", "39"))
 ms = ra.synthetic_mixture_set(5000, 160, D, seed=2024)
 opt = os.environ.get("OPT", "")
@@ -30,7 +32,8 @@ sc = ra.Scorer(ms, kind, max_frames=F, split_tile16=opt == "split16", split_tile
                full_keys=opt == "fullkeys")
 fr = torch.from_numpy(ra.synthetic_frames(F, D, seed=5)).cuda()
 out = torch.empty((5000, F), dtype=torch.float32, device="cuda")
-best = (torch.zeros((5000, F), dtype=torch.int32, device="cuda") if mode not in ("bint", "simds") else None)
+best = (torch.zeros((5000, F), dtype=torch.int32, device="cuda")
+        if mode not in ("bint", "simds", "fp32s", "pint", "pfloat") else None)
 for _ in range(3): sc.score_device(fr, out, best)
 torch.cuda.synchronize(); sc.set_timing(True)
 for _ in range(int(os.environ["STEPS"])): sc.score_device(fr, out, best)

@@ -26,6 +26,6 @@ while [ $# -ge 3 ]; do
   defs=$(echo "$i8 $f32" | tr ' ' '\n' | grep '^-D' | tr '\n' ' ')
   /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -ffp-contract=off -Ibuild $defs -c rasr_amd/csrc/gmm_api.cc -o build/variants/api_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o rasr_amd/lib/variants/librasr_gmm_$name.so \
-      build/variants/i8_$name.o build/variants/f32_$name.o build/variants/split_$name.o build/variants/api_$name.o $OTHER -lz -pthread -lrccl
+      build/variants/i8_$name.o build/variants/f32_$name.o build/variants/split_$name.o build/variants/api_$name.o $OTHER -lz -pthread -ldl
   echo built $name
 done

@@ -6,6 +6,7 @@
 #   smoke   : __graft_entry__.smoke()
 #   bench   : python bench.py (BENCH_ARGS appended)
 #   prof    : rocprofv3 --kernel-trace --stats over bench.py (BENCH_ARGS appended)
+#   ab-MODE : scripts/ab_bench.py --mode MODE over AB_LIBS (default: the variant libraries), AB_ARGS appended
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${RUN:-session}
 mkdir -p "$OUT"
@@ -26,6 +27,7 @@ for s in ${STEPS:-pytest smoke}; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 900 python bench.py ${BENCH_ARGS} ;;
     prof)   step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py ${BENCH_ARGS} ;;
+    ab-*)   step "$s" 900 python scripts/ab_bench.py --mode "${s#ab-}" ${AB_ARGS} ${AB_LIBS:-rasr_amd/lib/variants/*.so} ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
