@@ -7,6 +7,8 @@
 #   bench   : python bench.py (BENCH_ARGS appended)
 #   prof    : rocprofv3 --kernel-trace --stats over bench.py (BENCH_ARGS appended)
 #   ab-MODE : scripts/ab_bench.py --mode MODE over AB_LIBS (default: the variant libraries), AB_ARGS appended
+#   pmc-MODE: scripts/profile_pmc.sh MODE (one rocprofv3 --pmc pass per counter group, gpurun_out/pmc_MODE)
+#   line-X  : one other bench line, timed alone (X: sum sums d45 d45s pint pfloat nn ragged)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${RUN:-session}
 mkdir -p "$OUT"
@@ -28,6 +30,15 @@ for s in ${STEPS:-pytest smoke}; do
     bench)  step bench 900 python bench.py ${BENCH_ARGS} ;;
     prof)   step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py ${BENCH_ARGS} ;;
     ab-*)   step "$s" 900 python scripts/ab_bench.py --mode "${s#ab-}" ${AB_ARGS} ${AB_LIBS:-rasr_amd/lib/variants/*.so} ;;
+    pmc-*)  step "$s" 1000 bash scripts/profile_pmc.sh "${s#pmc-}" ;;
+    line-*)
+      B="--gpus 1 --steps 20 --warmup 3 --cpu-baseline off --host-boundary off --extras off --no-extra-mode"
+      case ${s#line-} in
+        sum) A="--mode sum" ;; sums) A="--mode sum --no-best" ;; d45) A="--dim 45" ;;
+        d45s) A="--dim 45 --mode simd-scores" ;; pint) A="--mode presel-int" ;; pfloat) A="--mode presel-float" ;;
+        nn) A="--mode nn" ;; ragged) A="--ragged" ;; *) echo "unknown line $s"; exit 2 ;;
+      esac
+      step "$s" 300 python bench.py $A $B ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
