@@ -213,4 +213,8 @@ clean:
 	rm -rf $(BUILD) $(LIBDIR)
 	$(MAKE) -C oracle clean
 
+# make -s print-VAR: a variable's value (scripts/build_variants.sh takes the per-TU kernel flags from here)
+print-%:
+	@echo '$($*)'
+
 .PHONY: all oracle clean check-integration check-integration-link

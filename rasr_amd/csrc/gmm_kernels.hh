@@ -88,14 +88,16 @@ struct F32Args {
 };
 
 #ifndef GMM_SPLIT_NF
-#define GMM_SPLIT_NF 4  // the split kernel is written for 4 (emitMixtureSplit)
+#define GMM_SPLIT_NF 8  // 4 or 8 (A/B builds)
 #endif
-constexpr int      kSplitNF             = GMM_SPLIT_NF;  // column blocks of 16 frames per wave, split kernel
-#ifndef GMM_SPLIT_WAVES
-#define GMM_SPLIT_WAVES 4
-#endif
-constexpr uint32_t kSplitWaves          = GMM_SPLIT_WAVES;  // waves per workgroup of the split kernels
-constexpr uint32_t kSplitFramesPerBlock = kSplitWaves * kSplitNF * 16;
+// scoreSplit (diagonal-maximum, batch-float): column blocks of 16 frames per wave.  At 8 (128 frames per wave,
+// one wave per SIMD, the frame operands in the accumulator file) every tile fragment a wave loads feeds twice
+// the MFMAs of 4, and the pair step's VALU is the epilogue alone: 4.68 against 5.35 ms per 32768 frames, A/B.
+constexpr int      kSplitNF             = GMM_SPLIT_NF;
+constexpr uint32_t kSplitFramesPerBlock = 256;  // frames per workgroup of every split kernel
+constexpr uint32_t kSplitWaves          = kSplitFramesPerBlock / 64;  // 64 frames per wave: scoreSplit32,
+                                                                      // scoreSplitSum, preselection-batch-float
+constexpr uint32_t kSplitMainWaves      = kSplitFramesPerBlock / (16 * kSplitNF);  // scoreSplit
 
 constexpr uint32_t kSplitLimbs   = 4;
 constexpr uint32_t kSplitXXLimbs = 3;

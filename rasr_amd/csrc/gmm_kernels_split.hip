@@ -231,9 +231,11 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
 extern __shared__ __attribute__((aligned(16))) uint32_t splitSelLds[];
 
 template <int KS, bool BEST, bool PRESEL>
-__global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
+__global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
                                                                       const uint32_t* __restrict__ mixTileOff) {
-    constexpr int  NF   = 4;
+    constexpr int  NF   = PRESEL ? 4 : kSplitNF;  // 4 or 8 column blocks; the emit works on halves of 4
+    constexpr int  NH   = NF / 4;
+    static_assert(NF == 4 || NF == 8, "64 or 128 frames per wave");
     const int      lane = threadIdx.x & 63;
     const int      wave = threadIdx.x >> 6;
     const uint32_t g    = static_cast<uint32_t>(lane) >> 4;
@@ -283,16 +285,24 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
 #pragma unroll
         for (int s = 0; s < KS; ++s)
             B[cb][s] = fh[(static_cast<size_t>(fb0 + cb) * KS + s) * 64 + lane];
-    const int eOut = a.frameExp[frame0 + lane];  // exponent of the frame this lane stores
+    int eOut[NH];  // exponents of the frames this lane stores (frame0 + 64 h + lane)
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+        eOut[h] = a.frameExp[frame0 + 64u * h + lane];
     // wait for the frame operands here, before the tile prefetch is issued: otherwise the waitcnt pass
     // sees them possibly pending at the loop header and drains the whole queue there every iteration
 #pragma unroll
     for (int cb = 0; cb < NF; ++cb) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-            asm volatile("" ::"v"(B[cb][s]));
+            if constexpr (NF == 8)  // loop-invariant MFMA operands: to the accumulator file (VGPRs: the epilogue)
+                asm volatile("" : "+a"(B[cb][s]));
+            else
+                asm volatile("" ::"v"(B[cb][s]));
     }
-    asm volatile("" ::"v"(eOut));
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+        asm volatile("" ::"v"(eOut[h]));
 
     // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
     f16x8 R0[KS], R1[KS], R2[KS], R3[KS];
@@ -374,7 +384,10 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
     const auto emit = [&]() {
-        emitMixtureSplit<BEST>(a, best, m, frame0, lane, g, kmask, eOut, noneScore, 0.5f);
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            emitMixtureSplit<BEST>(a, *reinterpret_cast<const uint32_t(*)[4][4]>(&best[4 * h]), m, frame0 + 64u * h,
+                                   lane, g, kmask, eOut[h], noneScore, 0.5f);
     };
     // after an emit at tile tNext: next mixture, and the empty ones that also end there (rare path)
     const auto advance = [&](uint32_t tNext) {
@@ -390,7 +403,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     // one pipeline step: the MFMAs of the pair in (A0, A1) into cur beside the epilogue of the pair in
     // prev, interleaved 1 MFMA : 2 VALU (the operand loads for two pairs ahead follow, then finish())
     // (PRESEL: the mask words of the pair in (C0w, C1w) are read into TTcur; TTprev are prev's)
-    constexpr int kIl = PRESEL ? 28 : GMM_SPLIT_IL, kIlV = PRESEL ? 3 : 2;
+    constexpr int kIl = PRESEL ? 28 : GMM_SPLIT_IL * NH, kIlV = PRESEL ? 3 : 2;
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
                           const f32x4(&prev)[2][NF], uint32_t tPrev, const uint2& C0w, const uint2& C1w,
                           uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) {
@@ -404,7 +417,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, kIlV, 0);  // VALU
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 32 - kIl, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NF * KS - kIl, 0);
     };
     // the emit of the mixture that ended at tile tNext, if any (a separate block: with the emit inside
     // the interleaved one, the duplicated step needs more than 256 VGPRs)
@@ -990,9 +1003,11 @@ static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
                            a.mixTileOff);
     }
     else if (a.best)
-        hipLaunchKernelGGL((dev::scoreSplit<KS, true, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit<KS, true, false>), dim3(grid), dim3(64 * kSplitMainWaves), 0, s, a,
+                           a.mixTileOff);
     else
-        hipLaunchKernelGGL((dev::scoreSplit<KS, false, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit<KS, false, false>), dim3(grid), dim3(64 * kSplitMainWaves), 0, s, a,
+                           a.mixTileOff);
 }
 
 template <int KS>
