@@ -42,6 +42,9 @@
 #ifndef GMM_SPLIT_IL
 #define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
 #endif
+#ifndef GMM_SPLIT_SUM_NF
+#define GMM_SPLIT_SUM_NF 4  // diagonal-sum: column blocks of 16 frames per wave (4 or 8)
+#endif
 #ifndef GMM_SPLIT_TAG_EMIT
 #define GMM_SPLIT_TAG_EMIT 0  // 1: a tile's keys carry (tile << 2) only; the slot r is OR-ed in at the mixture's end
 #endif
@@ -742,9 +745,10 @@ __device__ __forceinline__ void emitMixtureSplitSum(const SplitArgs& a, const ui
 }
 
 template <int KS, bool BEST>
-__global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(SplitArgs a,
-                                                                         const uint32_t* __restrict__ mixTileOff) {
-    constexpr int  NF   = 4;
+__global__ __launch_bounds__(kSplitFramesPerBlock / GMM_SPLIT_SUM_NF * 4, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(
+        SplitArgs a, const uint32_t* __restrict__ mixTileOff) {
+    constexpr int  NF   = GMM_SPLIT_SUM_NF;  // 4 or 8 column blocks; the emit works on halves of 4
+    constexpr int  NH   = NF / 4;
     constexpr int  KH   = KS / 2;  // k-steps issued beside the first half of the epilogue
     const int      lane = threadIdx.x & 63;
     const int      wave = threadIdx.x >> 6;
@@ -776,8 +780,12 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
 #pragma unroll
     for (int cb = 0; cb < NF; ++cb) {
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
-            asm volatile("" ::"v"(B[cb][s]));
+        for (int s = 0; s < KS; ++s) {
+            if constexpr (NF == 8)
+                asm volatile("" : "+a"(B[cb][s]));
+            else
+                asm volatile("" ::"v"(B[cb][s]));
+        }
         asm volatile("" ::"v"(kap[cb]));
     }
     // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
@@ -806,7 +814,14 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     };
     uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
-    const auto emit    = [&]() { emitMixtureSplitSum<BEST>(a, best, S, Rf, m, frame0, lane, g, kmask); };
+    const auto emit = [&]() {
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            emitMixtureSplitSum<BEST>(a, *reinterpret_cast<const uint32_t(*)[4][2]>(&best[4 * h]),
+                                      *reinterpret_cast<const float(*)[4][2]>(&S[4 * h]),
+                                      *reinterpret_cast<const float(*)[4]>(&Rf[4 * h]), m, frame0 + 64u * h, lane, g,
+                                      kmask);
+    };
     const auto advance = [&](uint32_t tNext) {
         ++m;
         tBeg = tNext;
@@ -1057,9 +1072,11 @@ hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps16
 template <int KS>
 static void launchSplitSumK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
     if (a.best)
-        hipLaunchKernelGGL((dev::scoreSplitSum<KS, true>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplitSum<KS, true>), dim3(grid), dim3(kSplitFramesPerBlock / GMM_SPLIT_SUM_NF * 4), 0,
+                           s, a, a.mixTileOff);
     else
-        hipLaunchKernelGGL((dev::scoreSplitSum<KS, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplitSum<KS, false>), dim3(grid), dim3(kSplitFramesPerBlock / GMM_SPLIT_SUM_NF * 4),
+                           0, s, a, a.mixTileOff);
 }
 
 hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream) {
