@@ -282,6 +282,11 @@ int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
 #ifndef GMM_TARGET_BLOCKS
 #define GMM_TARGET_BLOCKS 8192
 #endif
+#ifndef GMM_SPLIT_TARGET_BLOCKS
+// the split kernels' cap: fewer, longer chunks reload a wave's 128 frame operands less often (A/B at 32768 frames:
+// 2048 -> 4.653 ms, 4096 -> 4.700, 8192 -> 4.753; at 8192 frames 1.299 / 1.309 / 1.318, profiles/r04/s13)
+#define GMM_SPLIT_TARGET_BLOCKS 2048
+#endif
     // RASR_GMM_TARGET_BLOCKS: tuning override (scripts/sweep_chunks.sh, scripts/sweep_small_batches.sh)
     static const uint32_t kOverride = [] {
         const char* e = std::getenv("RASR_GMM_TARGET_BLOCKS");
@@ -294,7 +299,9 @@ int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
     // frames 0.0695 with 2048 vs 0.0729); large calls keep GMM_TARGET_BLOCKS
     const uint32_t kTargetBlocks =
             kOverride ? kOverride
-            : s->split ? std::clamp<uint32_t>(nFrameTiles * 256u, 1024u, uint32_t(GMM_TARGET_BLOCKS))
+            : s->split ? std::clamp<uint32_t>(nFrameTiles * 256u, 1024u,
+                                              s->flavor == Flavor::DiagonalSum ? uint32_t(GMM_TARGET_BLOCKS)  // 64-frame waves:
+                                                                               : uint32_t(GMM_SPLIT_TARGET_BLOCKS))  // 8192 (A/B)
             : s->quantized && !s->presel ? std::clamp<uint32_t>(nFrameTiles * 1024u, 2048u, uint32_t(GMM_TARGET_BLOCKS))
                                          : uint32_t(GMM_TARGET_BLOCKS);
     uint32_t       target        = std::max<uint32_t>(1, (kTargetBlocks + nFrameTiles - 1) / nFrameTiles);
@@ -771,8 +778,87 @@ int transposeChunk(gmm_scorer* s, bool scores, bool best, uint32_t t0, uint32_t 
     return GMM_OK;
 }
 
+// Small calls (up to kSmallHostFrames frames: the drop-in's buffer sizes 1..64, RASR's default is 4) are bound by
+// their fixed cost, not by PCIe bandwidth: the pipeline below spends two copy-engine transfers, two cross-stream
+// events and two synchronizations on a few kilobytes.  With a page-locked ring and page-locked tables mapped at
+// the same address on the device (gmm_host_alloc, hipHostMalloc), such a call runs on one stream with no copy
+// engine: a kernel gathers the frame rows from the ring, the scorer runs as for any call, and the transpose (frame
+// major) or a strided copy kernel (mixture major) stores the tables straight into the caller's rows over PCIe;
+// one synchronization.  RASR_GMM_SMALL_HOST=0 turns it off (A/B).
+constexpr uint32_t kSmallHostFrames = 64;
+
+bool smallHostPathEnabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RASR_GMM_SMALL_HOST");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+void keepBestOf(gmm_scorer* s, const HostRing& r, const std::vector<HostSegment>& segs, bool frameMajor, bool lazyBest) {
+    s->keptBestCall   = s->hostCall;
+    s->keptRing       = r;
+    s->keptSegs       = segs;
+    s->keptFrameMajor = frameMajor;
+    s->keptLazy       = lazyBest;
+    s->keptComputed   = !lazyBest;
+}
+
+int scoreHostSmall(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, uint32_t scoreStride, bool keepBest,
+                   bool lazyBest, bool frameMajor, bool async) {
+    const uint32_t nFrames = r.nFrames, M = s->nMix;
+    int            rc      = ensureHostPipeline(s, 1);
+    if (rc != GMM_OK)
+        return rc;
+    std::vector<HostSegment> segs;
+    appendSegments(r, 0, 0, nFrames, segs);
+    const uint32_t D = s->D;
+    GMM_HIP_CHECK(hipEventRecord(s->hostStart, nullptr));
+    GMM_HIP_CHECK(hipStreamWaitEvent(s->hostCompute, s->hostStart, 0));
+    for (const HostSegment& g : segs)
+        GMM_HIP_CHECK(launchCopyWords2D(reinterpret_cast<const uint32_t*>(r.frames + static_cast<size_t>(g.col) * r.frameStride),
+                                        r.frameStride, reinterpret_cast<uint32_t*>(s->dHostFrames + static_cast<size_t>(g.t0) * D),
+                                        D, g.n, D, s->hostCompute));
+    const bool withBest = best || (keepBest && !lazyBest);
+    if ((rc = scoreImpl(s, s->dHostFrames, nFrames, D, s->dHostScores, withBest ? s->dHostBest : nullptr, nFrames,
+                        s->hostCompute)) != GMM_OK)
+        return rc;
+    struct Table {
+        uint32_t*       dst;
+        const uint32_t* src;
+    };
+    for (Table t : {Table{reinterpret_cast<uint32_t*>(scores), reinterpret_cast<const uint32_t*>(s->dHostScores)},
+                    Table{best, s->dHostBest}}) {
+        if (!t.dst)
+            continue;
+        for (const HostSegment& g : segs) {
+            if (frameMajor)
+                GMM_HIP_CHECK(launchTransposeWords(t.src + g.t0, M, g.n, nFrames, t.dst + static_cast<size_t>(g.col) * scoreStride,
+                                                   scoreStride, s->hostCompute));
+            else
+                GMM_HIP_CHECK(launchCopyWords2D(t.src + g.t0, nFrames, t.dst + g.col, scoreStride, M, g.n, s->hostCompute));
+        }
+    }
+    if (keepBest)  // gmm_fetch_best_density's copies wait for this call's scorer
+        GMM_HIP_CHECK(hipEventRecord(s->chunkDone[0], s->hostCompute));
+    if (async) {
+        if (!s->asyncDone)
+            GMM_HIP_CHECK(hipEventCreateWithFlags(&s->asyncDone, hipEventDisableTiming));
+        GMM_HIP_CHECK(hipEventRecord(s->asyncDone, s->hostCompute));
+        s->asyncCall = s->hostCall;
+    }
+    else
+        GMM_HIP_CHECK(hipStreamSynchronize(s->hostCompute));
+    if (keepBest)
+        keepBestOf(s, r, segs, frameMajor, lazyBest);
+    return GMM_OK;
+}
+
 int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* best, uint32_t scoreStride, bool keepBest,
                   bool lazyBest, bool frameMajor, bool async) {
+    if (r.nFrames <= kSmallHostFrames && !s->presel && !s->group && smallHostPathEnabled() && isDeviceMappedHost(r.frames) &&
+        isDeviceMappedHost(scores) && (!best || isDeviceMappedHost(best)))
+        return scoreHostSmall(s, r, scores, best, scoreStride, keepBest, lazyBest, frameMajor, async);
     const uint32_t fpb = framesPerBlock(s), nFrames = r.nFrames;
     // frame chunks for large tables; one chunk for preselection (gmm_scorer_cluster_selection reports the
     // last call's whole batch)
@@ -817,14 +903,8 @@ int scoreHostImpl(gmm_scorer* s, const HostRing& r, float* scores, uint32_t* bes
     }
     else
         GMM_HIP_CHECK(hipStreamSynchronize(s->hostCompute));
-    if (keepBest) {
-        s->keptBestCall  = s->hostCall;
-        s->keptRing      = r;
-        s->keptSegs      = segs;
-        s->keptFrameMajor = frameMajor;
-        s->keptLazy       = lazyBest;
-        s->keptComputed   = !lazyBest;
-    }
+    if (keepBest)
+        keepBestOf(s, r, segs, frameMajor, lazyBest);
     return GMM_OK;
 }
 

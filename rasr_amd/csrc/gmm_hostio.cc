@@ -79,4 +79,13 @@ bool isPinnedHost(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
+bool isDeviceMappedHost(const void* p) {
+    hipPointerAttribute_t a{};
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer == p;
+}
+
 }  // namespace rasr_gmm

@@ -47,4 +47,8 @@ unsigned hostCopyThreads();
 // hipHostRegister / gmm_host_alloc), i.e. the DMA engines can write it directly
 bool isPinnedHost(const void* p);
 
+// true when p is page-locked host memory that kernels can address at p itself (hipHostMalloc / gmm_host_alloc
+// on ROCm: the same virtual address on host and device), so a kernel reads and writes it over PCIe
+bool isDeviceMappedHost(const void* p);
+
 }  // namespace rasr_gmm

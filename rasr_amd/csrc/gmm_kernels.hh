@@ -198,6 +198,8 @@ hipError_t launchMinShardKeys(const int64_t* slots, uint32_t nSlots, size_t n, i
 hipError_t launchMinIntoShardKeys(int64_t* dst, const int64_t* src, size_t n, hipStream_t stream);
 
 // frame-major host tables (gmm_kernels_layout.hip): dst[c * dstPitch + r] = src[r * srcPitch + c], 32-bit words
+hipError_t launchCopyWords2D(const uint32_t* src, uint32_t srcPitch, uint32_t* dst, uint32_t dstPitch, uint32_t rows,
+                             uint32_t cols, hipStream_t stream);
 hipError_t launchTransposeWords(const uint32_t* src, uint32_t rows, uint32_t cols, uint32_t srcPitch, uint32_t* dst,
                                 uint32_t dstPitch, hipStream_t stream);
 

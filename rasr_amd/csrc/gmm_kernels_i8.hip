@@ -42,23 +42,28 @@ namespace dev {
 // frame preparation (quantized): Context::Context, SimdFeatureScorer.cc:22-35
 //   frameQ [C][nFramesPad][KS*64] s8 (q - 128, 0 in the padding), frameSS [C][nFramesPad] = sum (q-128)^2
 // ---------------------------------------------------------------------------
+// 32 threads per (covariance, frame), 8 per 256-thread block: thread t quantizes the 16-byte block t of the
+// frame's KS x 64 bytes (KS <= 8) and the frame's sum of squares is a shuffle sum (integer: any order).  One
+// thread per frame walking the bytes serially took most of a small host call's preparation time.
 __global__ __launch_bounds__(256) void prepareFramesI8(const float* __restrict__ frames, uint32_t nFrames,
                                                         uint32_t frameStride, uint32_t nFramesPad,
                                                         uint32_t nFramesRead, uint32_t D,
                                                         uint32_t C, uint32_t KS, const float* __restrict__ isv,
                                                         int8_t* __restrict__ frameQ, int32_t* __restrict__ frameSS) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= C * nFramesRead)
-        return;
-    const uint32_t c = gid / nFramesRead, f = gid % nFramesRead;
+    const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 5), blk = threadIdx.x & 31u;
+    if (g >= C * nFramesRead)
+        return;  // whole 32-thread groups leave together
+    const uint32_t c = g / nFramesRead, f = g % nFramesRead;
     const float*   x  = frames + static_cast<size_t>(f) * frameStride;
     const float*   iv = isv + static_cast<size_t>(c) * KS * 64;
     i32x4*         out = reinterpret_cast<i32x4*>(frameQ + (static_cast<size_t>(c) * nFramesPad + f) * KS * 64);
     int            ss = 0;
-    for (uint32_t blk = 0; blk < KS * 4; ++blk) {
+    if (blk < KS * 4) {
         i32x4 w;
+#pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
             uint32_t word = 0;
+#pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const uint32_t k = blk * 16 + q4 * 4 + b;
                 int            v = 0;
@@ -72,7 +77,11 @@ __global__ __launch_bounds__(256) void prepareFramesI8(const float* __restrict__
         }
         out[blk] = w;
     }
-    frameSS[static_cast<size_t>(c) * nFramesPad + f] = ss;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)
+        ss += __shfl_xor(ss, o, 32);
+    if (blk == 0)
+        frameSS[static_cast<size_t>(c) * nFramesPad + f] = ss;
 }
 
 // ---------------------------------------------------------------------------
@@ -863,8 +872,8 @@ using dev::prepareFramesI8;
 hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesPad,
                                  uint32_t nFramesRead, uint32_t D, uint32_t C, uint32_t KS, const float* isv,
                                  int8_t* frameQ, int32_t* frameSS, hipStream_t stream) {
-    const uint32_t n = C * nFramesRead;
-    hipLaunchKernelGGL(prepareFramesI8, dim3((n + 255) / 256), dim3(256), 0, stream, frames, nFrames, frameStride,
+    const uint32_t n = C * nFramesRead;  // (covariance, frame) pairs, 8 per block
+    hipLaunchKernelGGL(prepareFramesI8, dim3((n + 7) / 8), dim3(256), 0, stream, frames, nFrames, frameStride,
                        nFramesPad, nFramesRead, D, C, KS, isv, frameQ, frameSS);
     return hipGetLastError();
 }

@@ -9,6 +9,8 @@
 // 2 x 4 B per (frame, mixture) at a few TB/s) and copies contiguous frame rows over PCIe.
 #include "gmm_device.hh"
 
+#include <algorithm>
+
 namespace rasr_gmm {
 namespace dev {
 
@@ -34,7 +36,34 @@ __global__ __launch_bounds__(256) void transposeWords(const uint32_t* __restrict
     }
 }
 
+// dst[r * dstPitch + c] = src[r * srcPitch + c] for r < rows, c < cols (32-bit words): the small host calls' frame
+// gather from a page-locked ring and table stores into page-locked caller tables (either side may be host memory
+// mapped for the device; one row per 64-lane group, so a row's words go out as whole 256-byte bursts)
+__global__ __launch_bounds__(256) void copyWords2D(const uint32_t* __restrict__ src, uint32_t srcPitch,
+                                                   uint32_t* __restrict__ dst, uint32_t dstPitch, uint32_t rows,
+                                                   uint32_t cols) {
+    if (srcPitch == cols && dstPitch == cols) {  // one contiguous run (e.g. one frame's mixture-major column)
+        const size_t n = static_cast<size_t>(rows) * cols;
+        for (size_t i = static_cast<size_t>(blockIdx.x) * 256u + threadIdx.x; i < n; i += static_cast<size_t>(gridDim.x) * 256u)
+            dst[i] = src[i];
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6); r < rows; r += gridDim.x * 4u)
+        for (uint32_t c = lane; c < cols; c += 64u)
+            dst[static_cast<size_t>(r) * dstPitch + c] = src[static_cast<size_t>(r) * srcPitch + c];
+}
+
 }  // namespace dev
+
+hipError_t launchCopyWords2D(const uint32_t* src, uint32_t srcPitch, uint32_t* dst, uint32_t dstPitch, uint32_t rows,
+                             uint32_t cols, hipStream_t stream) {
+    if (rows == 0 || cols == 0)
+        return hipSuccess;
+    const uint32_t blocks = std::min<uint32_t>((rows + 3u) / 4u, 1024u);
+    hipLaunchKernelGGL(dev::copyWords2D, dim3(blocks), dim3(256), 0, stream, src, srcPitch, dst, dstPitch, rows, cols);
+    return hipGetLastError();
+}
 
 hipError_t launchTransposeWords(const uint32_t* src, uint32_t rows, uint32_t cols, uint32_t srcPitch, uint32_t* dst,
                                 uint32_t dstPitch, hipStream_t stream) {

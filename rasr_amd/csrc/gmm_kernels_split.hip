@@ -68,9 +68,13 @@ __device__ __forceinline__ uint16_t h16bits(float v) {
 }
 
 // ---------------------------------------------------------------------------
-// frame preparation: one thread per frame
+// frame preparation: 32 threads per frame, 8 frames per 256-thread block
 //   frameH  [nFramesPad/16][KS16][64][8] f16 (B fragments), frameXX = ||x'||^2 * 2^-e,
 //   frameExp = e.  Rows >= nFrames are zero.
+// The frame's x' go to LDS once (lane t of the frame's 32 takes d = t, t + 32, ...), the exponent from a
+// shuffle max, ||x'||^2 in the reference's sequential order by the frame's first thread, then every thread
+// builds its 8-value groups of K.  (One thread per frame walking K serially took 22 us for a 1-frame call,
+// most of a small host call's device time: profiles/r04/s14.)
 // ---------------------------------------------------------------------------
 template <int ROWS>
 __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restrict__ frames, uint32_t nFrames,
@@ -81,35 +85,56 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
                                                            const int32_t* __restrict__ limbExp,
                                                            u32x4* __restrict__ frameH, float* __restrict__ frameXX,
                                                            int32_t* __restrict__ frameExp) {
-    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= nFramesRead)
-        return;
-    const bool   valid = f < nFrames;
-    const float* x     = frames + static_cast<size_t>(f) * frameStride;
-    float        xx = 0.0f, ymax = 0.0f;
-    bool         finite = true;
+    __shared__ float xs[8][128];  // x' of the block's frames (D <= 126)
+    __shared__ float shXX[8];
+    __shared__ int   shE[8];
+    const uint32_t   fl = threadIdx.x >> 5, t = threadIdx.x & 31u;
+    const uint32_t   f       = blockIdx.x * 8u + fl;
+    const bool       inRange = f < nFramesRead, valid = f < nFrames;
+    const float*     x       = frames + static_cast<size_t>(f) * frameStride;
+    float            ymax    = 0.0f;
+    int              finite  = 1;
     if (valid)
-        for (uint32_t k = 0; k < D; ++k) {
+        for (uint32_t k = t; k < D; k += 32u) {
             const float v = __fmul_rn(__fsub_rn(x[k], centre[k]), isv[k]);  // x' as the f32 kernel forms it
-            xx            = __fadd_rn(xx, __fmul_rn(v, v));
+            xs[fl][k]     = v;
             const float y = fabsf(v * dimScale[k]);
             finite        = finite && y <= 3.40282347e+38f;
             ymax          = fmaxf(ymax, y);
         }
-    int e = 0;
-    if (finite && ymax > 32768.0f) {
-        int ex;
-        frexpf(ymax, &ex);  // ymax in [2^(ex-1), 2^ex)
-        e = ex - 15;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        ymax   = fmaxf(ymax, __shfl_xor(ymax, o, 32));
+        finite = finite & __shfl_xor(finite, o, 32);
     }
-    if (finite && xx < 3.40282347e+38f && ldexpf(xx, -e) >= 1073741824.0f) {  // ||x'||^2 2^-e < 2^30 (its top limb)
-        int ex;
-        frexpf(xx, &ex);
-        e = ex - 30;
+    __syncthreads();
+    if (t == 0 && inRange) {
+        float xx = 0.0f;
+        if (valid)
+            for (uint32_t k = 0; k < D; ++k)
+                xx = __fadd_rn(xx, __fmul_rn(xs[fl][k], xs[fl][k]));
+        int e = 0;
+        if (finite && ymax > 32768.0f) {
+            int ex;
+            frexpf(ymax, &ex);  // ymax in [2^(ex-1), 2^ex)
+            e = ex - 15;
+        }
+        if (finite && xx < 3.40282347e+38f && ldexpf(xx, -e) >= 1073741824.0f) {  // ||x'||^2 2^-e < 2^30 (its top limb)
+            int ex;
+            frexpf(xx, &ex);
+            e = ex - 30;
+        }
+        const float xxs = ldexpf(xx, -e);
+        frameXX[f]      = xxs;
+        frameExp[f]     = e;
+        shXX[fl]        = xxs;
+        shE[fl]         = e;
     }
-    const float xxs = ldexpf(xx, -e);
-    frameXX[f]      = xxs;
-    frameExp[f]     = e;
+    __syncthreads();
+    if (!inRange)
+        return;
+    const int   e   = shE[fl];
+    const float xxs = shXX[fl];
     // ||x'||^2 2^-e as three f16 limbs against 2^15, 2^4, 2^-7 on the model side
     uint16_t xxl[kSplitXXLimbs];
     {
@@ -124,7 +149,7 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
     // B fragments: 16 rows: frame block f/16, lane 16*((k>>3)&3) + f%16, step k>>5;
     //              32 rows: frame block f/32, lane 32*((k>>3)&1) + f%32, step k>>4
     const uint32_t fb = f / ROWS, col = f % ROWS;
-    for (uint32_t q = 0; q < KS16 * (ROWS == 32 ? 2 : 4); ++q) {  // groups of 8 consecutive k
+    for (uint32_t q = t; q < KS16 * (ROWS == 32 ? 2 : 4); q += 32u) {  // groups of 8 consecutive k
         uint32_t w[4] = {0, 0, 0, 0};
         if (valid)
             for (uint32_t j = 0; j < 8; ++j) {
@@ -132,7 +157,7 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
                 uint16_t       h = 0;
                 if (k < 3 * D) {
                     const uint32_t d  = k < D ? k : (k < 2 * D ? k - D : k - 2 * D);
-                    const float    y  = ldexpf(__fmul_rn(__fsub_rn(x[d], centre[d]), isv[d]) * dimScale[d], -e);
+                    const float    y  = ldexpf(xs[fl][d] * dimScale[d], -e);
                     const uint16_t hi = h16bits(y);
                     h = (k >= D && k < 2 * D) ? h16bits(y - static_cast<float>(__builtin_bit_cast(_Float16, hi))) : hi;
                 }
@@ -998,11 +1023,11 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream) {
     if (rows == 32)
-        hipLaunchKernelGGL(dev::prepareFramesSplit<32>, dim3((nFramesRead + 255) / 256), dim3(256), 0, stream, frames,
+        hipLaunchKernelGGL(dev::prepareFramesSplit<32>, dim3((nFramesRead + 7) / 8), dim3(256), 0, stream, frames,
                            nFrames, frameStride, nFramesRead, D, kSteps, isv, centre, dimScale, limbExp,
                            static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
     else
-        hipLaunchKernelGGL(dev::prepareFramesSplit<16>, dim3((nFramesRead + 255) / 256), dim3(256), 0, stream, frames,
+        hipLaunchKernelGGL(dev::prepareFramesSplit<16>, dim3((nFramesRead + 7) / 8), dim3(256), 0, stream, frames,
                            nFrames, frameStride, nFramesRead, D, kSteps, isv, centre, dimScale, limbExp,
                            static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
     return hipGetLastError();

@@ -1,6 +1,7 @@
 // GpuFeatureScorer.cc -- see GpuFeatureScorer.hh.
 #include "GpuFeatureScorer.hh"
 
+#include <algorithm>
 #include <cassert>
 #include <cstdio>
 #include <cstdlib>
@@ -252,7 +253,8 @@ private:
 struct GpuFeatureScorer::Slot {
     HostTable<float>    scores;  // [nMixtures]
     HostTable<uint32_t> best;    // [nMixtures]
-    std::vector<float>  frame;   // the frame, for scoring it again
+    HostTable<float>    frame;   // [dimension] the frame (page-locked: the library's small-call path reads it
+                                 // on the device), kept for scoring it again
     std::vector<float>  scratch; // scores of that second scoring (the context keeps its first ones)
     uint64_t            call = 0;
     bool                bestValid = false;
@@ -292,10 +294,11 @@ Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
     else {
         slot.reset(new Slot());
         const size_t n = std::max<uint32_t>(nMixtures_, 1);
-        if (!slot->scores.allocate(n, 0.0f) || (assigning_ && !slot->best.allocate(n, 0xffffffffu)))
+        if (!slot->scores.allocate(n, 0.0f) || (assigning_ && !slot->best.allocate(n, 0xffffffffu)) ||
+            !slot->frame.allocate(std::max<uint32_t>(dimension_, 1), 0.0f))
             criticalError("gmm_host_alloc");
     }
-    slot->frame.assign(f.begin(), f.end());
+    std::copy(f.begin(), f.end(), slot->frame.data());
     ++launches_;
     if (gmm_score_host_ring(handle_, slot->frame.data(), 1, 0, 1, dimension_, slot->scores.data(), nullptr, 1,
                             assigning_ ? GMM_HOST_LAZY_BEST : 0u, &slot->call) != GMM_OK)
