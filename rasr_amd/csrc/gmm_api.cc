@@ -261,6 +261,17 @@ uint32_t framesPerBlock(const gmm_scorer* s) {
     return s->split ? kSplitFramesPerBlock : kF32FramesPerBlock;
 }
 
+// the frame tile of one call: the quantized kernels take 256-frame tiles for calls of up to 256 frames
+bool i8SmallTile(const gmm_scorer* s, uint32_t nFrames) {
+    return s->quantized && !s->presel && nFrames <= kI8SmallFrames;
+}
+
+uint32_t framesPerBlock(const gmm_scorer* s, uint32_t nFrames) {
+    if (i8SmallTile(s, nFrames))
+        return kI8SmallFrames;
+    return framesPerBlock(s);
+}
+
 // the selection of every frame of the call: mask words for whole 64-frame blocks (padding frames too)
 int selectClustersFor(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nPadCall,
                       hipStream_t stream) {
@@ -382,7 +393,7 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         return groupScore(s, frames, nFrames, frameStride, scores, best, scoreStride, stream);
     if (!best && s->scoresOnly)
         return scoreImpl(s->scoresOnly.get(), frames, nFrames, frameStride, scores, nullptr, scoreStride, stream);
-    const uint32_t fpb         = framesPerBlock(s);
+    const uint32_t fpb         = framesPerBlock(s, nFrames);
     const uint32_t nFrameTiles = (nFrames + fpb - 1) / fpb;
     const uint32_t nPadCall    = nFrameTiles * fpb;  // rows the scorer reads
     const ChunkTable* ct       = nullptr;
@@ -426,6 +437,7 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.nClusters   = s->clustering.nClusters;
         a.mixOddMask  = s->dMixOddMask;
         a.scoreOnly   = s->scoreOnly ? 1 : 0;
+        a.smallTile   = i8SmallTile(s, nFrames) ? 1 : 0;
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         GMM_HIP_CHECK(launchScoreI8(a, s->kSteps, s->multiCov, stream));

@@ -38,6 +38,7 @@ constexpr int      kI8NF          = GMM_I8_NF;   // column blocks of 16 frames p
 constexpr int      kF32NF         = GMM_F32_NF;  // column blocks of 16 frames per wave, float kernel
 constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kI8FramesPerBlock  = kWavesPerBlock * kI8NF * 16;   // 512
+constexpr uint32_t kI8SmallFrames     = kWavesPerBlock * 4 * 16;        // 256: the small-call tile (I8Args::smallTile)
 constexpr uint32_t kF32FramesPerBlock = kWavesPerBlock * kF32NF * 16;  // 256
 constexpr uint32_t kFramePadQuantum   = 512;
 constexpr uint32_t kTilePad           = 16;   // zero tiles after the last one (prefetch / LDS segments)
@@ -67,6 +68,9 @@ struct I8Args {
     // MFMA's C input, mixOddMask[m] bit g = lane group g holds odd-Q rows
     const uint32_t* mixOddMask;
     int             scoreOnly;
+    // small calls (<= kI8SmallFrames frames, no preselection): 64 frames per wave, 256 per workgroup -- a
+    // 1..256-frame call computes half the padded frames of the 128-frame waves
+    int             smallTile;
 };
 
 struct F32Args {

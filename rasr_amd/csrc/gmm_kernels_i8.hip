@@ -926,7 +926,14 @@ hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStr
         return hipErrorInvalidValue;
     if (a.scoreOnly && (multiCov || kSteps != 1 || !GMM_I8_LDS || !a.mixOddMask))
         return hipErrorInvalidValue;
-    if (kSteps == 1)
+    if (a.smallTile && a.presel)
+        return hipErrorInvalidValue;  // the preselection kernels keep their frame tile
+    // small calls: 64-frame waves (I8Args::smallTile)
+    if (kSteps == 1 && a.smallTile)
+        multiCov ? launchI8T<4, 1, true>(a, grid, stream) : launchI8T<4, 1, false>(a, grid, stream);
+    else if (kSteps == 2 && a.smallTile)
+        multiCov ? launchI8T<4, 2, true>(a, grid, stream) : launchI8T<4, 2, false>(a, grid, stream);
+    else if (kSteps == 1)
         multiCov ? launchI8T<kI8NF, 1, true>(a, grid, stream) : launchI8T<kI8NF, 1, false>(a, grid, stream);
     else if (kSteps == 2)
         multiCov ? launchI8T<kI8NF, 2, true>(a, grid, stream) : launchI8T<kI8NF, 2, false>(a, grid, stream);

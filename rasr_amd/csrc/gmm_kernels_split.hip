@@ -42,6 +42,9 @@
 #ifndef GMM_SPLIT_IL
 #define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
 #endif
+#ifndef GMM_SPLIT_DIAG_NOEMIT
+#define GMM_SPLIT_DIAG_NOEMIT 0
+#endif
 #ifndef GMM_SPLIT_SUM_NF
 #define GMM_SPLIT_SUM_NF 4  // diagonal-sum: column blocks of 16 frames per wave (4 or 8)
 #endif
@@ -49,7 +52,7 @@
 #define GMM_SPLIT_TAG_EMIT 0  // 1: a tile's keys carry (tile << 2) only; the slot r is OR-ed in at the mixture's end
 #endif
 #ifndef GMM_SPLIT_EMIT_FLAT
-#define GMM_SPLIT_EMIT_FLAT 0  // 1: the emit's finalize without the exec-mask branch around the no-candidate case
+#define GMM_SPLIT_EMIT_FLAT 1  // the emit finalize without the exec-mask branch (A/B at 128 frames per wave: -0.25..-0.5 %)
 #endif
 
 namespace rasr_gmm {
@@ -194,6 +197,20 @@ template <bool BEST>
 __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][4], uint32_t m,
                                                  uint32_t frame0, int lane, uint32_t g, uint32_t kmask, int eOut,
                                                  float noneScore, float halfScale) {
+#if GMM_SPLIT_DIAG_NOEMIT  // diagnostic (wrong results): the emit's cost, the minima kept live by one XOR chain
+    {
+        uint32_t x = 0;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                x ^= best[cb][r];
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(m - a.mixBase) * a.scoreStride,
+                                                         (short)0, static_cast<int>(a.nFrames * 4u), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(x, rs, static_cast<uint32_t>(frame0 + lane) * 4u, 0, GMM_STORE_CPOL);
+        return;
+    }
+#endif
     uint32_t k[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
