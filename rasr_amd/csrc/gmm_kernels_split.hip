@@ -36,11 +36,17 @@
 // minimum is a float key whose low tileBits mantissa bits hold the tile number.
 #include "gmm_device.hh"
 
+#include <type_traits>
+#include <utility>
+
 #ifndef GMM_SPLIT_MIN_WAVES
 #define GMM_SPLIT_MIN_WAVES 1
 #endif
 #ifndef GMM_SPLIT_IL
 #define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
+#endif
+#ifndef GMM_SPLIT_PF
+#define GMM_SPLIT_PF 2  // tile pairs in flight per wave (scoreSplit without preselection; 3: +2.6 % at D = 39, profiles/r04/s18)
 #endif
 #ifndef GMM_SPLIT_DIAG_NOEMIT
 #define GMM_SPLIT_DIAG_NOEMIT 0
@@ -60,6 +66,15 @@ namespace dev {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int... I, class F>
+__device__ __forceinline__ void staticForImpl(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void staticFor(F&& f) {  // f(integral_constant<int, i>) for i = 0 .. N-1, in order
+    staticForImpl(std::make_integer_sequence<int, N>{}, f);
+}
 
 __device__ __forceinline__ uint32_t umin3(uint32_t x, uint32_t y, uint32_t z) {
     return min(min(x, y), z);  // v_min3_u32
@@ -313,7 +328,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
             Cw = tclu[static_cast<size_t>(tt) * 4 + g];  // rows 4g .. 4g+3: cluster * 64, u16 each
     };
     // the mask words of a tile's 4 rows in this lane (column frame0 + 16 cb + (lane & 15), byte cb)
-    const auto readSel = [&](const uint2& Cw, uint32_t(&T)[4]) {
+    const auto readSel = [&](const uint2& Cw, uint32_t(&T)[4]) __attribute__((always_inline)) {
         if constexpr (PRESEL) {
             const char* base = reinterpret_cast<const char*>(splitSelLds) + laneSel;
             T[0]             = *reinterpret_cast<const uint32_t*>(base + (Cw.x & 0xffffu));
@@ -350,12 +365,18 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
         asm volatile("" ::"v"(eOut[h]));
 
     // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
-    f16x8 R0[KS], R1[KS], R2[KS], R3[KS];
-    uint2 C0{0, 0}, C1{0, 0}, C2{0, 0}, C3{0, 0};
-    loadTile(T0, R0, C0);
-    loadTile(T0 + 1, R1, C1);
-    loadTile(T0 + 2, R2, C2);
-    loadTile(T0 + 3, R3, C3);
+    // operand registers of PF pairs in flight: pair j (counted from T0) in set j % PF, loaded when pair j - PF has
+    // been issued.  One wave per SIMD at 128 frames per wave: nothing else covers a late tile, so three pairs
+    // (3 x 2 x KS f16x8) are in flight there
+    constexpr int PF = (PRESEL || KS > 5) ? 2 : GMM_SPLIT_PF;  // K steps 6-8: registers
+    f16x8         R[PF][2][KS];
+    uint2         C[PF][2];
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+        C[j][0] = C[j][1] = uint2{0, 0};
+        loadTile(T0 + 2 * j, R[j][0], C[j][0]);
+        loadTile(T0 + 2 * j + 1, R[j][1], C[j][1]);
+    }
 
     // scores only (no best density, no preselection mask): keys are the values' own bits, nothing masked
     const uint32_t kmask = (BEST || PRESEL) ? (1u << a.tileBits) - 1u : 0u;
@@ -379,7 +400,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
             for (int r = 0; r < kSlots; ++r)
                 best[cb][r] = 0xffffffffu;
     };
-    const auto chain = [&](const f16x8(&A)[KS], f32x4(&acc)[NF]) {
+    const auto chain = [&](const f16x8(&A)[KS], f32x4(&acc)[NF]) __attribute__((always_inline)) {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
             acc[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};  // ||x'||^2 is in K: the chain starts from an inline 0
@@ -390,7 +411,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
                 acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
     };
     // epilogue of one pair of tiles (tile numbers tl, tl + 1 in the mixture); TT: their mask words
-    const auto pairEpilogue = [&](const f32x4(&acc)[2][NF], uint32_t tl, const uint32_t(&TT)[2][4]) {
+    const auto pairEpilogue = [&](const f32x4(&acc)[2][NF], uint32_t tl, const uint32_t(&TT)[2][4]) __attribute__((always_inline)) {
         // per-slot tags as opaque SGPRs: with a visible constant the compiler splits the tag OR off the
         // v_and_or_b32 into a v_and + v_or3 pair (non-volatile asm: no scheduling barrier)
         uint32_t tagA[4], tagB[4];
@@ -428,14 +449,14 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
 
     uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
-    const auto emit = [&]() {
+    const auto emit = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int h = 0; h < NH; ++h)
             emitMixtureSplit<BEST>(a, *reinterpret_cast<const uint32_t(*)[4][4]>(&best[4 * h]), m, frame0 + 64u * h,
                                    lane, g, kmask, eOut[h], noneScore, 0.5f);
     };
     // after an emit at tile tNext: next mixture, and the empty ones that also end there (rare path)
-    const auto advance = [&](uint32_t tNext) {
+    const auto advance = [&](uint32_t tNext) __attribute__((always_inline)) {
         ++m;
         tBeg = tNext;
         tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
@@ -451,7 +472,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
     constexpr int kIl = PRESEL ? 28 : GMM_SPLIT_IL * NH, kIlV = PRESEL ? 3 : 2;
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
                           const f32x4(&prev)[2][NF], uint32_t tPrev, const uint2& C0w, const uint2& C1w,
-                          uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) {
+                          uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) __attribute__((always_inline)) {
         chain(A0, cur[0]);
         chain(A1, cur[1]);
         readSel(C0w, TTcur[0]);
@@ -466,7 +487,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
     };
     // the emit of the mixture that ended at tile tNext, if any (a separate block: with the emit inside
     // the interleaved one, the duplicated step needs more than 256 VGPRs)
-    const auto finish = [&](uint32_t tNext) {
+    const auto finish = [&](uint32_t tNext) __attribute__((always_inline)) {
         if (tNext == tEnd) {
             emit();
             resetBest();
@@ -474,7 +495,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
         }
     };
     // the last pair's epilogue (nothing left to overlap it with)
-    const auto drain = [&](const f32x4(&prev)[2][NF], uint32_t tPrev, const uint32_t(&TTprev)[2][4]) {
+    const auto drain = [&](const f32x4(&prev)[2][NF], uint32_t tPrev, const uint32_t(&TTprev)[2][4]) __attribute__((always_inline)) {
         pairEpilogue(prev, tPrev - tBeg, TTprev);
         finish(tPrev + 2);
     };
@@ -486,34 +507,43 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
         tEnd = m < m1 ? mixTileOff[m + 1] : T0;
     }
     if (T0 < T1) {
-        f32x4    accX[2][NF], accY[2][NF];
-        uint32_t TTX[2][4] = {}, TTY[2][4] = {};
-        uint32_t t = T0;
-        chain(R0, accX[0]);  // pair 0: nothing to finish beside it
-        chain(R1, accX[1]);
-        readSel(C0, TTX[0]);
-        readSel(C1, TTX[1]);
-        loadTile(t + 4, R0, C0);
-        loadTile(t + 5, R1, C1);
-        t += 2;
-        for (; t + 4 <= T1; t += 4) {
-            step(R2, R3, accY, accX, t - 2, C2, C3, TTY, TTX);
-            loadTile(t + 4, R2, C2);
-            loadTile(t + 5, R3, C3);
-            finish(t);
-            step(R0, R1, accX, accY, t, C0, C1, TTX, TTY);
-            loadTile(t + 6, R0, C0);
-            loadTile(t + 7, R1, C1);
-            finish(t + 2);
-        }
-        if (t < T1) {  // one more pair (in R2, R3)
-            step(R2, R3, accY, accX, t - 2, C2, C3, TTY, TTX);
-            finish(t);
-            drain(accY, t, TTY);
-        }
-        else {
-            drain(accX, t - 2, TTX);
-        }
+        // pair j: accumulators acc[j % 2] (step j reads pair j - 1's from the other set), operands R[j % PF];
+        // the loop body is lcm(2, PF) pairs so that every index is a compile-time constant
+        constexpr int U = PF % 2 == 0 ? PF : 2 * PF;
+        f32x4         acc[2][2][NF];
+        uint32_t      TT[2][2][4] = {};
+        chain(R[0][0], acc[0][0]);  // pair 0: nothing to finish beside it
+        chain(R[0][1], acc[0][1]);
+        readSel(C[0][0], TT[0][0]);
+        readSel(C[0][1], TT[0][1]);
+        loadTile(T0 + 2 * PF, R[0][0], C[0][0]);
+        loadTile(T0 + 2 * PF + 1, R[0][1], C[0][1]);
+        uint32_t t = T0 + 2;  // first tile of pair 1
+        // sub-step i of a loop iteration: pair j = 1 + i (mod U) at tile tt
+        const auto sub = [&](auto ic, uint32_t tt) __attribute__((always_inline)) {
+            constexpr int i = decltype(ic)::value, set = (1 + i) % PF, cur = (1 + i) % 2, prv = i % 2;
+            step(R[set][0], R[set][1], acc[cur], acc[prv], tt - 2, C[set][0], C[set][1], TT[cur], TT[prv]);
+            loadTile(tt + 2 * PF, R[set][0], C[set][0]);  // the tile array is padded by kTilePad >= 2 PF tiles
+            loadTile(tt + 2 * PF + 1, R[set][1], C[set][1]);
+            finish(tt);
+        };
+        for (; t + 2 * U <= T1; t += 2 * U)
+            staticFor<U>([&](auto ic) __attribute__((always_inline)) { sub(ic, t + 2u * decltype(ic)::value); });
+        // fewer than U pairs left, then the last pair's epilogue
+        bool live = true;
+        staticFor<U>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int  i  = decltype(ic)::value;
+            const uint32_t tt = t + 2u * i;
+            if (live) {
+                if (tt < T1) {
+                    sub(ic, tt);
+                }
+                else {
+                    drain(acc[i % 2], tt - 2, TT[i % 2]);
+                    live = false;
+                }
+            }
+        });
     }
 }
 
