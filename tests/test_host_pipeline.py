@@ -168,6 +168,46 @@ def test_ring_matches_device(gpu, model, kind, R, first, n, pinned, keep_best, f
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum", "diagonal-sum"])
+@pytest.mark.parametrize("R,first,n", [(1, 0, 1), (7, 5, 6), (64, 63, 2), (64, 10, 30), (96, 40, 64)])
+@pytest.mark.parametrize("keep_best", [False, True, "lazy"])
+@pytest.mark.parametrize("frame_major", [False, True])
+def test_small_call_page_locked_ring(gpu, model, kind, R, first, n, keep_best, frame_major):
+    """Calls of up to 64 frames with a page-locked ring and page-locked tables take the one-stream path
+    (scoreHostSmall: the gather kernel reads the ring, the transpose / strided copy kernels write the caller's
+    rows over PCIe): bit-identical to gmm_score_device in ring order, wrapped or not, everything else untouched."""
+    ring = ra.pinned_empty((R, 33), np.float32)
+    ring[:] = ra.synthetic_frames(R, 33, seed=R + first + 1)
+    sc = ra.Scorer(model, kind, max_frames=64)
+    _ring_case(sc, ring, first, n, True, keep_best, frame_major)
+
+
+@pytest.mark.gpu
+def test_small_call_async_page_locked(gpu, model):
+    """GMM_HOST_ASYNC on the small-call path: the call's event is on the one stream; a later call and
+    gmm_host_call_wait both see the tables complete."""
+    R = 16
+    ring = ra.pinned_empty((R, 33), np.float32)
+    ring[:] = ra.synthetic_frames(R, 33, seed=5)
+    sc = ra.Scorer(model, "diagonal-maximum", max_frames=64)
+    m = sc.n_mixtures()
+    sync = np.zeros((R, m), np.float32)
+    sc.score_host_ring(ring, 0, R, sync, frame_major=True)
+    outs = [ra.pinned_empty((R, m), np.float32) for _ in range(3)]
+    ids = []
+    for i, o in enumerate(outs):  # back to back: each call waits for the previous one by itself
+        o[:] = -1.0
+        ids.append(sc.score_host_ring(ring, 4 * i, 4, o, frame_major=True, asynchronous=True))
+    sc.wait(ids[-1])
+    for i, o in enumerate(outs):
+        pos = np.arange(4 * i, 4 * i + 4)
+        assert np.array_equal(o[pos].view(np.uint32), sync[pos].view(np.uint32))
+        rest = np.ones(R, bool)
+        rest[pos] = False
+        assert (o[rest] == -1.0).all()
+
+
+@pytest.mark.gpu
 def test_fetch_best_after_later_call_is_refused(gpu, model):
     ring = ra.synthetic_frames(16, 33, seed=3)
     sc = ra.Scorer(model, "SIMD-diagonal-maximum", max_frames=16)
