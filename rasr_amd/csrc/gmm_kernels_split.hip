@@ -45,6 +45,11 @@
 #ifndef GMM_SPLIT_IL
 #define GMM_SPLIT_IL 24  // MFMAs of a pipeline step interleaved with kIlV VALU each (sched_group_barrier)
 #endif
+#ifndef GMM_SPLIT_PRESEL_NF
+#define GMM_SPLIT_PRESEL_NF 8  // preselection-batch-float: column blocks per wave (8: -6.7 % at D = 39, -9.6 % at 45, profiles/r04/s21)
+#endif
+// preselection-batch-float's column blocks per wave at K steps KS (8 spills beyond 5 K steps)
+constexpr int splitPreselNF(int ks) { return GMM_SPLIT_PRESEL_NF == 8 && ks <= 5 ? 8 : 4; }
 #ifndef GMM_SPLIT_PF
 #define GMM_SPLIT_PF 2  // tile pairs in flight per wave (scoreSplit without preselection; 3: +2.6 % at D = 39, profiles/r04/s18)
 #endif
@@ -291,9 +296,9 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
 extern __shared__ __attribute__((aligned(16))) uint32_t splitSelLds[];
 
 template <int KS, bool BEST, bool PRESEL>
-__global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
+__global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) * 4 : 64 * kSplitMainWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit(SplitArgs a,
                                                                       const uint32_t* __restrict__ mixTileOff) {
-    constexpr int  NF   = PRESEL ? 4 : kSplitNF;  // 4 or 8 column blocks; the emit works on halves of 4
+    constexpr int  NF   = PRESEL ? splitPreselNF(KS) : kSplitNF;  // 4 or 8 column blocks; the emit works on halves of 4
     constexpr int  NH   = NF / 4;
     static_assert(NF == 4 || NF == 8, "64 or 128 frames per wave");
     const int      lane = threadIdx.x & 63;
@@ -307,15 +312,15 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
     const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
 
-    // preselection: this wave's 64-frame mask table [cluster][16] into LDS (each wave reads only its own)
-    uint32_t laneSel = 0;  // byte address of (wave table, column t = lane & 15)
+    // preselection: this wave's NH 64-frame mask tables [cluster][16] into LDS (each wave reads only its own)
+    uint32_t laneSel = 0, selWords = 0;  // byte address of (wave's first table, column t = lane & 15); table words
     if constexpr (PRESEL) {
-        const uint32_t words = a.nClusters * 16u;
-        const u32x4*   src   = reinterpret_cast<const u32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
-        u32x4*         dst   = reinterpret_cast<u32x4*>(splitSelLds + static_cast<uint32_t>(wave) * words);
-        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u)
+        selWords = a.nClusters * 16u;
+        const u32x4* src = reinterpret_cast<const u32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * selWords);
+        u32x4*       dst = reinterpret_cast<u32x4*>(splitSelLds + static_cast<uint32_t>(wave) * NH * selWords);
+        for (uint32_t i = static_cast<uint32_t>(lane); i < NH * selWords / 4u; i += 64u)
             dst[i] = src[i];
-        laneSel = (static_cast<uint32_t>(wave) * words + (static_cast<uint32_t>(lane) & 15u)) * 4u;
+        laneSel = (static_cast<uint32_t>(wave) * NH * selWords + (static_cast<uint32_t>(lane) & 15u)) * 4u;
     }
     const uint2* tclu = static_cast<const uint2*>(a.tileClu);
 
@@ -327,14 +332,18 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
         if constexpr (PRESEL)
             Cw = tclu[static_cast<size_t>(tt) * 4 + g];  // rows 4g .. 4g+3: cluster * 64, u16 each
     };
-    // the mask words of a tile's 4 rows in this lane (column frame0 + 16 cb + (lane & 15), byte cb)
-    const auto readSel = [&](const uint2& Cw, uint32_t(&T)[4]) __attribute__((always_inline)) {
+    // the mask words of a tile's 4 rows in this lane: T[h][r] of row 4g + r, column frame0 + 64 h + 16 cb +
+    // (lane & 15) in byte cb
+    const auto readSel = [&](const uint2& Cw, uint32_t(&T)[NH][4]) __attribute__((always_inline)) {
         if constexpr (PRESEL) {
-            const char* base = reinterpret_cast<const char*>(splitSelLds) + laneSel;
-            T[0]             = *reinterpret_cast<const uint32_t*>(base + (Cw.x & 0xffffu));
-            T[1]             = *reinterpret_cast<const uint32_t*>(base + (Cw.x >> 16));
-            T[2]             = *reinterpret_cast<const uint32_t*>(base + (Cw.y & 0xffffu));
-            T[3]             = *reinterpret_cast<const uint32_t*>(base + (Cw.y >> 16));
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                const char* base = reinterpret_cast<const char*>(splitSelLds) + laneSel + h * selWords * 4u;
+                T[h][0]          = *reinterpret_cast<const uint32_t*>(base + (Cw.x & 0xffffu));
+                T[h][1]          = *reinterpret_cast<const uint32_t*>(base + (Cw.x >> 16));
+                T[h][2]          = *reinterpret_cast<const uint32_t*>(base + (Cw.y & 0xffffu));
+                T[h][3]          = *reinterpret_cast<const uint32_t*>(base + (Cw.y >> 16));
+            }
         }
     };
 
@@ -411,7 +420,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
                 acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
     };
     // epilogue of one pair of tiles (tile numbers tl, tl + 1 in the mixture); TT: their mask words
-    const auto pairEpilogue = [&](const f32x4(&acc)[2][NF], uint32_t tl, const uint32_t(&TT)[2][4]) __attribute__((always_inline)) {
+    const auto pairEpilogue = [&](const f32x4(&acc)[2][NF], uint32_t tl, const uint32_t(&TT)[2][NH][4]) __attribute__((always_inline)) {
         // per-slot tags as opaque SGPRs: with a visible constant the compiler splits the tag OR off the
         // v_and_or_b32 into a v_and + v_or3 pair (non-volatile asm: no scheduling barrier)
         uint32_t tagA[4], tagB[4];
@@ -431,8 +440,8 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
                 if constexpr (PRESEL) {
                     // tag | sign-extended mask byte (one v_or_b32_sdwa), made opaque so that the key stays
                     // one v_and_or_b32 (else the three ORs fold into v_or3 beside a separate v_and + v_bfe)
-                    uint32_t ca = tagA[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[0][r] >> (8 * cb))));
-                    uint32_t cc = tagB[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[1][r] >> (8 * cb))));
+                    uint32_t ca = tagA[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[0][cb / 4][r] >> (8 * (cb % 4)))));
+                    uint32_t cc = tagB[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[1][cb / 4][r] >> (8 * (cb % 4)))));
                     asm("" : "+v"(ca), "+v"(cc));
                     best[cb][r] = umin3(best[cb][r], (__float_as_uint(acc[0][cb][r]) & vmask) | ca,
                                         (__float_as_uint(acc[1][cb][r]) & vmask) | cc);
@@ -469,10 +478,10 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
     // one pipeline step: the MFMAs of the pair in (A0, A1) into cur beside the epilogue of the pair in
     // prev, interleaved 1 MFMA : 2 VALU (the operand loads for two pairs ahead follow, then finish())
     // (PRESEL: the mask words of the pair in (C0w, C1w) are read into TTcur; TTprev are prev's)
-    constexpr int kIl = PRESEL ? 28 : GMM_SPLIT_IL * NH, kIlV = PRESEL ? 3 : 2;
+    constexpr int kIl = PRESEL ? 28 * NH : GMM_SPLIT_IL * NH, kIlV = PRESEL ? 3 : 2;
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
                           const f32x4(&prev)[2][NF], uint32_t tPrev, const uint2& C0w, const uint2& C1w,
-                          uint32_t(&TTcur)[2][4], const uint32_t(&TTprev)[2][4]) __attribute__((always_inline)) {
+                          uint32_t(&TTcur)[2][NH][4], const uint32_t(&TTprev)[2][NH][4]) __attribute__((always_inline)) {
         chain(A0, cur[0]);
         chain(A1, cur[1]);
         readSel(C0w, TTcur[0]);
@@ -495,7 +504,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
         }
     };
     // the last pair's epilogue (nothing left to overlap it with)
-    const auto drain = [&](const f32x4(&prev)[2][NF], uint32_t tPrev, const uint32_t(&TTprev)[2][4]) __attribute__((always_inline)) {
+    const auto drain = [&](const f32x4(&prev)[2][NF], uint32_t tPrev, const uint32_t(&TTprev)[2][NH][4]) __attribute__((always_inline)) {
         pairEpilogue(prev, tPrev - tBeg, TTprev);
         finish(tPrev + 2);
     };
@@ -511,7 +520,7 @@ __global__ __launch_bounds__(PRESEL ? 64 * kSplitWaves : 64 * kSplitMainWaves, G
         // the loop body is lcm(2, PF) pairs so that every index is a compile-time constant
         constexpr int U = PF % 2 == 0 ? PF : 2 * PF;
         f32x4         acc[2][2][NF];
-        uint32_t      TT[2][2][4] = {};
+        uint32_t      TT[2][2][NH][4] = {};
         chain(R[0][0], acc[0][0]);  // pair 0: nothing to finish beside it
         chain(R[0][1], acc[0][1]);
         readSel(C[0][0], TT[0][0]);
@@ -1083,11 +1092,12 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
 template <int KS>
 static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
     if (a.presel) {  // preselection-batch-float: no best density; the waves' mask tables in dynamic LDS
-        const uint32_t lds = kSplitWaves * a.nClusters * 64u;
+        // the block's 256 frames = 4 tables of [clusters][16] words, whatever the waves
+        const uint32_t lds = kSplitFramesPerBlock / 64u * a.nClusters * 64u;
         (void)allowDynamicLds(reinterpret_cast<const void*>(&dev::scoreSplit<KS, false, true>),
-                              static_cast<int>(kSplitWaves * 256u * 64u));
-        hipLaunchKernelGGL((dev::scoreSplit<KS, false, true>), dim3(grid), dim3(64 * kSplitWaves), lds, s, a,
-                           a.mixTileOff);
+                              static_cast<int>(kSplitFramesPerBlock / 64u * 256u * 64u));
+        hipLaunchKernelGGL((dev::scoreSplit<KS, false, true>), dim3(grid), dim3(kSplitFramesPerBlock / splitPreselNF(KS) * 4),
+                           lds, s, a, a.mixTileOff);
     }
     else if (a.best)
         hipLaunchKernelGGL((dev::scoreSplit<KS, true, false>), dim3(grid), dim3(64 * kSplitMainWaves), 0, s, a,
