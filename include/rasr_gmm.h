@@ -176,7 +176,11 @@ int gmm_score_host(gmm_scorer* scorer, const float* frames, uint32_t n_frames, u
  *   gmm_fetch_best_density then computes the best densities from them (one more scoring pass over the call's
  *   frames, whose scores are not copied again).  The reference likewise evaluates bestDensity(e) only when
  *   asked (AssigningFeatureScorer.hh:110-121): a search that reads only score(e) never pays for the
- *   assignment. */
+ *   assignment.
+ * Small calls (n_frames <= 64, e.g. a recognizer's buffer of 1..64 frames) whose ring and tables all come from
+ *   gmm_host_alloc run on one stream without the copy engine: a kernel reads the ring rows and the tables are
+ *   written by kernels over PCIe (about 80 us instead of 125 us for one frame at 800k densities, DESIGN.md
+ *   section 4).  Other buffers take the copy-engine path; the results are bit-identical either way. */
 #define GMM_HOST_LAZY_BEST 4u
 /* flags: GMM_HOST_ASYNC: the call returns once its copies and kernels are enqueued; its tables are written when
  *   gmm_host_call_wait(scorer, call_id) returns (or any later host call of the scorer, which waits for it
