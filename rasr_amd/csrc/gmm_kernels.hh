@@ -98,7 +98,10 @@ struct F32Args {
 // one wave per SIMD, the frame operands in the accumulator file) every tile fragment a wave loads feeds twice
 // the MFMAs of 4, and the pair step's VALU is the epilogue alone: 4.68 against 5.35 ms per 32768 frames, A/B.
 constexpr int      kSplitNF             = GMM_SPLIT_NF;
-constexpr uint32_t kSplitFramesPerBlock = 256;  // frames per workgroup of every split kernel
+#ifndef GMM_SPLIT_FPB
+#define GMM_SPLIT_FPB 256
+#endif
+constexpr uint32_t kSplitFramesPerBlock = GMM_SPLIT_FPB;  // frames per workgroup of every split kernel (A/B: 512)
 constexpr uint32_t kSplitWaves          = kSplitFramesPerBlock / 64;  // 64 frames per wave: scoreSplit32,
                                                                       // scoreSplitSum, preselection-batch-float
 constexpr uint32_t kSplitMainWaves      = kSplitFramesPerBlock / (16 * kSplitNF);  // scoreSplit
