@@ -31,8 +31,8 @@
 // A[row l&15][k = 8(l>>4) + j] and B[k = 8(l>>4) + j][col l&15], j = 0..7; C/D hold
 // col l&15, rows 4(l>>4) + r.
 //
-// Work decomposition and epilogue are the f32 kernel's (gmm_kernels_f32.hip): a workgroup is
-// 4 waves x NF column blocks of 16 frames walking a chunk of mixtures on one XCD; the running
+// Work decomposition and epilogue follow the f32 kernel's (gmm_kernels_f32.hip): a workgroup's waves
+// hold NF column blocks of 16 frames each and walk a chunk of mixtures on one XCD; the running
 // minimum is a float key whose low tileBits mantissa bits hold the tile number.
 #include "gmm_device.hh"
 
@@ -280,19 +280,22 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
 }
 
 // ---------------------------------------------------------------------------
-// scorer.  A workgroup = 4 waves x 64 frames (4 column blocks of 16) walks a chunk of mixtures on one
-// XCD.  Every mixture has an even number of tiles (host), so the chunk is a flat sequence of tile
-// pairs.  Operands of consecutive pairs alternate between two register sets (R0,R1 / R2,R3) loaded
-// two pairs ahead, and the pipeline is software-staged: step p issues the 32 MFMAs of pair p beside
-// the epilogue (tag + min) of pair p-1, interleaved MFMA : VALU by sched_group_barrier, then emits the
-// mixture that pair p-1 ended, if any.  Mixture bounds are scalar
+// scorer.  A workgroup of 256 frames = 2 waves x 128 frames (8 column blocks of 16; preselection and
+// K steps > 5 as noted below) walks a chunk of mixtures on one XCD.  The 128 frames' f16 fragments are
+// loop-invariant MFMA B operands and live in the accumulator file (an "a"-constrained asm pins them),
+// the accumulators in VGPRs, one wave per SIMD.  Every mixture has an even number of tiles (host), so the
+// chunk is a flat sequence of tile pairs.  Operands of PF consecutive pairs rotate through PF register
+// sets loaded PF pairs ahead, and the pipeline is software-staged: step p issues the 64 MFMAs of pair p
+// beside the epilogue (tag + min) of pair p-1, interleaved MFMA : VALU by sched_group_barrier, then emits
+// the mixture that pair p-1 ended, if any.  Mixture bounds are scalar
 // loads (mixTileOff is a restrict kernel argument): a vector load there would come with an
 // s_waitcnt vmcnt(0) draining the prefetch.
 // ---------------------------------------------------------------------------
 // PRESEL (preselection-batch-float): every key is OR-ed with the sign-extended mask byte of its
 // (frame, density cluster), so a density whose cluster the frame did not select becomes the all-ones
-// key and never wins; the wave's mask table (gmm_kernels_presel.hip) sits in LDS, a tile carries the
-// 16 rows' table offsets, and a pair's 8 mask words are read in the step that issues its MFMAs.
+// key and never wins; the wave's mask tables (one per 64 frames, gmm_kernels_presel.hip) sit in LDS, a
+// tile carries the 16 rows' table offsets, and a pair's mask words are read in the step that issues its
+// MFMAs.
 extern __shared__ __attribute__((aligned(16))) uint32_t splitSelLds[];
 
 template <int KS, bool BEST, bool PRESEL>
@@ -373,10 +376,9 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
     for (int h = 0; h < NH; ++h)
         asm volatile("" ::"v"(eOut[h]));
 
-    // the tile array is padded by kTilePad >= 4 tiles: prefetching past T1 stays in bounds
     // operand registers of PF pairs in flight: pair j (counted from T0) in set j % PF, loaded when pair j - PF has
-    // been issued.  One wave per SIMD at 128 frames per wave: nothing else covers a late tile, so three pairs
-    // (3 x 2 x KS f16x8) are in flight there
+    // been issued (the tile array is padded by kTilePad >= 2 PF tiles: prefetching past T1 stays in bounds).
+    // PF = 2; 3 measured 2.6 % slower at 128 frames per wave (GMM_SPLIT_PF)
     constexpr int PF = (PRESEL || KS > 5) ? 2 : GMM_SPLIT_PF;  // K steps 6-8: registers
     f16x8         R[PF][2][KS];
     uint2         C[PF][2];
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
         }
     };
     // one pipeline step: the MFMAs of the pair in (A0, A1) into cur beside the epilogue of the pair in
-    // prev, interleaved 1 MFMA : 2 VALU (the operand loads for two pairs ahead follow, then finish())
+    // prev, interleaved 1 MFMA : 2 VALU (the operand loads for PF pairs ahead follow, then finish())
     // (PRESEL: the mask words of the pair in (C0w, C1w) are read into TTcur; TTprev are prev's)
     constexpr int kIl = PRESEL ? 28 * NH : GMM_SPLIT_IL * NH, kIlV = PRESEL ? 3 : 2;
     const auto step = [&](const f16x8(&A0)[KS], const f16x8(&A1)[KS], f32x4(&cur)[2][NF],
@@ -494,8 +496,8 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * NF * KS - kIl, 0);
     };
-    // the emit of the mixture that ended at tile tNext, if any (a separate block: with the emit inside
-    // the interleaved one, the duplicated step needs more than 256 VGPRs)
+    // the emit of the mixture that ended at tile tNext, if any, in a block of its own (inside the interleaved
+    // step it measured 9-11 % slower at 128 frames per wave)
     const auto finish = [&](uint32_t tNext) __attribute__((always_inline)) {
         if (tNext == tEnd) {
             emit();
