@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The hybrid-DNN forward pass of the bench (NN_DIMS, 32768 frames, bf16 operands, f32 accumulate) through
 PyTorch's own GEMMs (hipBLASLt on ROCm): torch.nn.functional.linear + sigmoid per hidden layer, the output
-layer's linear + log_softmax.  A yardstick for nnGemm8p's all-layer time (bench.py --mode nn), not a product path.
+layer's linear with the prior folded into its bias (as nnGemm8p: no softmax, the hybrid scorer's scores are the
+prior-corrected logits).  A yardstick for nnGemm8p's all-layer time (bench.py --mode nn), not a product path.
 usage: nn_torch_ref.py [--frames 32768] [--iters 20]"""
 import argparse
 import json
@@ -29,7 +30,7 @@ def main():
         for i, (w, b) in enumerate(zip(ws, bs)):
             h = torch.nn.functional.linear(h, w, b)
             if not gemm_only:
-                h = torch.sigmoid(h) if i < len(ws) - 1 else torch.log_softmax(h.float(), dim=1)
+                h = torch.sigmoid(h) if i < len(ws) - 1 else h.float()
         return h
 
     out = {}
