@@ -93,6 +93,7 @@ CASES = [
     (50, "ragged", 33, 333, 64, 6),
     (30, 5, 16, 130, 256, 32),      # 150 entries: clusters reduced to 150
     (80, 16, 45, 257, 128, 128),    # everything selected
+    (40, 8, 60, 200, 64, 8),        # float: 6 K steps, the 64-frame-wave kernel (128 frames per wave up to 5)
 ]
 
 
