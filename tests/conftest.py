@@ -11,6 +11,10 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
     config.addinivalue_line("markers", "slow: larger CPU cases")
+    # the oracle libraries are built with the reference's -ffast-math, whose startup code sets flush-to-zero /
+    # denormals-are-zero for the whole process, as in a RASR binary; numpy then reports a zero smallest subnormal
+    config.addinivalue_line("filterwarnings",
+                            "ignore:The value of the smallest subnormal for <class 'numpy.float64'> type is zero")
 
 
 @pytest.fixture(scope="session")
