@@ -261,15 +261,20 @@ uint32_t framesPerBlock(const gmm_scorer* s) {
     return s->split ? kSplitFramesPerBlock : kF32FramesPerBlock;
 }
 
-// the frame tile of one call: the quantized kernels take 256-frame tiles for calls of up to 256 frames
-bool i8SmallTile(const gmm_scorer* s, uint32_t nFrames) {
-    return s->quantized && !s->presel && nFrames <= kI8SmallFrames;
+// the frame tile of one call: the quantized kernels take 256-frame tiles for calls of up to 256 frames and
+// 64-frame ones (one wave per workgroup, one covariance) for calls of up to 64 (I8Args::smallTile)
+int i8SmallTile(const gmm_scorer* s, uint32_t nFrames) {
+    if (!s->quantized || s->presel || nFrames > kI8SmallFrames)
+        return 0;
+    return nFrames <= kI8TinyFrames && !s->multiCov ? 2 : 1;
 }
 
 uint32_t framesPerBlock(const gmm_scorer* s, uint32_t nFrames) {
-    if (i8SmallTile(s, nFrames))
-        return kI8SmallFrames;
-    return framesPerBlock(s);
+    switch (i8SmallTile(s, nFrames)) {
+        case 2: return kI8TinyFrames;
+        case 1: return kI8SmallFrames;
+        default: return framesPerBlock(s);
+    }
 }
 
 // the selection of every frame of the call: mask words for whole 64-frame blocks (padding frames too)
@@ -437,7 +442,7 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.nClusters   = s->clustering.nClusters;
         a.mixOddMask  = s->dMixOddMask;
         a.scoreOnly   = s->scoreOnly ? 1 : 0;
-        a.smallTile   = i8SmallTile(s, nFrames) ? 1 : 0;
+        a.smallTile   = i8SmallTile(s, nFrames);
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         GMM_HIP_CHECK(launchScoreI8(a, s->kSteps, s->multiCov, stream));

@@ -39,6 +39,7 @@ constexpr int      kF32NF         = GMM_F32_NF;  // column blocks of 16 frames p
 constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kI8FramesPerBlock  = kWavesPerBlock * kI8NF * 16;   // 512
 constexpr uint32_t kI8SmallFrames     = kWavesPerBlock * 4 * 16;        // 256: the small-call tile (I8Args::smallTile)
+constexpr uint32_t kI8TinyFrames      = 4 * 16;                         // 64: one 64-frame wave per workgroup
 constexpr uint32_t kF32FramesPerBlock = kWavesPerBlock * kF32NF * 16;  // 256
 constexpr uint32_t kFramePadQuantum   = 512;
 constexpr uint32_t kTilePad           = 16;   // zero tiles after the last one (prefetch / LDS segments)
@@ -68,8 +69,8 @@ struct I8Args {
     // MFMA's C input, mixOddMask[m] bit g = lane group g holds odd-Q rows
     const uint32_t* mixOddMask;
     int             scoreOnly;
-    // small calls (<= kI8SmallFrames frames, no preselection): 64 frames per wave, 256 per workgroup -- a
-    // 1..256-frame call computes half the padded frames of the 128-frame waves
+    // small calls (no preselection): 1 = 64 frames per wave, 256 per workgroup (<= kI8SmallFrames frames: half
+    // the padded frames of the 128-frame waves); 2 = one such wave per workgroup (<= kI8TinyFrames frames)
     int             smallTile;
 };
 

@@ -368,11 +368,12 @@ extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 // (word bits 16-31: the class tile count; bits 4-15: er): row 4g + r of mixed tile i has parity
 // (16 i + 4g + r >= er), and their candidates 2 v + p go to a second running minimum, merged at the mixture end.
 // A pair step holds two tiles of one kind.
-template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles, bool SCORE_ONLY = false>
-__global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_WAVES : 1) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
+template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles, bool SCORE_ONLY = false, int W = 4>
+__global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W == 4) ? GMM_I8_WAVES : 1) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
                                                    float* __restrict__ scores, uint32_t* __restrict__ bestOut,
                                                    const uint32_t* __restrict__ mixOddMask = nullptr) {
     static_assert(NF == 4 || NF == 8, "NF");
+    static_assert(W == 4 || (W == 1 && !PRESEL), "waves per workgroup: 4, or 1 for small calls (no preselection)");
     static_assert(!PRESEL || NF == 4 || NF == 8, "preselection masks: one or two 64-frame words per wave");
     // PRESEL mask table entries: NF 4 a byte (4 deselection bits x 4: the byte offset of a u32 in maskLut), NF 8 a
     // u16 (8 bits x 8: the byte offset of a u64 in maskLut)
@@ -386,9 +387,10 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     constexpr uint32_t kSegA     = kSegTiles * kTileA;
     constexpr uint32_t kSegP     = kSegA + kSegTiles * 64;      // + packed row constants
     constexpr uint32_t kSegBytes = kSegP + (PRESEL ? kSegTiles * 64 : 0);  // + row cluster offsets (u32)
-    constexpr int      kPieces   = kSegTiles * KS / 4;          // 1 KiB pieces per wave per segment
+    constexpr int      kPieces   = kSegTiles * KS / W;          // 1 KiB pieces per wave per segment
+    constexpr uint32_t kRowLanes = 4 * kSegTiles / W;           // lanes loading 16 B of row constants per wave
     constexpr int      kIssued   = kPieces + 1 + (PRESEL ? 1 : 0);  // vector memory ops per wave per segment
-    static_assert(kSegTiles * KS % 4 == 0, "segment pieces must split evenly over 4 waves");
+    static_assert(kSegTiles * KS % W == 0 && kRowLanes <= 64, "segment pieces must split evenly over the waves");
     // after the ring: the stand-in second tile of a step that has one tile left (odd tile count, segment
     // end): zero operands (dot = 0), rows that never win, cluster offsets 0.  Every step is then a pair
     // step: one loop body, whose running minima stay in their registers (a second, single-tile body made
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
     uint32_t  chunk, ft;
     if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
         return;  // uniform over the workgroup, before any barrier
-    const uint32_t frame0 = ft * (4u * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
+    const uint32_t frame0 = ft * (W * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
     const int      ib = static_cast<int>(a.idxBits);
     const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
@@ -435,9 +437,9 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
             __builtin_amdgcn_global_load_lds(gA + static_cast<size_t>(t0) * kTileA + piece * 1024u + lane * 16,
                                              base + piece * 1024u, 16, 0, 0);
         }
-        if (lane < kSegTiles)  // kSegTiles tiles x 64 B of row constants: 16 kSegTiles B per wave
-            __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * (kSegTiles * 16) + lane * 16,
-                                             base + kSegA + wave * (kSegTiles * 16), 16, 0, 0);
+        if (lane < kRowLanes)  // kSegTiles tiles x 64 B of row constants: 16 kRowLanes B per wave
+            __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * (kRowLanes * 16) + lane * 16,
+                                             base + kSegA + wave * (kRowLanes * 16), 16, 0, 0);
         if constexpr (PRESEL) {  // kSegTiles tiles x 64 B of row cluster offsets: 16 kSegTiles B per wave
             if (lane < kSegTiles)
                 __builtin_amdgcn_global_load_lds(gClu + static_cast<size_t>(t0) * 64 + wave * (kSegTiles * 16) + lane * 16,
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(256, (KS == 1 && !PRESEL && GMM_I8_WAVES) ? GMM_I8_
         // SCORE_ONLY: the class layout's padding value (2 v + 1 of a mixed step stays inside int32)
         const uint32_t never    = PRESEL ? 0xffffffffu : (SCORE_ONLY ? 0x30000000u : 0x7fffffffu);
         const uint32_t neverClu = PRESEL ? a.nClusters * 16u * kEntryBytes : 0u;  // u32 row offsets
-        for (uint32_t i = threadIdx.x; i < kDummyBytes / 4; i += 256u)
+        for (uint32_t i = threadIdx.x; i < kDummyBytes / 4; i += 64u * W)
             reinterpret_cast<uint32_t*>(dummy)[i] = (i >= kTileA / 4 && i < kTileA / 4 + 16)
                                                             ? never
                                                             : (i >= kTileA / 4 + 16 ? neverClu : 0u);
@@ -878,7 +880,7 @@ hipError_t launchPrepareFramesI8(const float* frames, uint32_t nFrames, uint32_t
     return hipGetLastError();
 }
 
-template <int NF, int KS, bool MULTI>
+template <int NF, int KS, bool MULTI, int W = 4>
 static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
 #if GMM_I8_LDS
     if constexpr (!MULTI) {
@@ -902,16 +904,18 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
                                a.mixTileOff, a.scores, a.best, nullptr);
             return;
         }
+        // 16-tile segments for one K step (34 KiB per workgroup, 4 per CU); 8 for two (also 34 KiB); one-wave
+        // workgroups take half of that (more of them per CU)
+        constexpr int kSeg = (KS == 1 ? dev::kSegTiles : 8) / (W == 1 ? 2 : 1);
         if constexpr (KS == 1) {
             if (a.scoreOnly) {  // batch types on the class layout
-                hipLaunchKernelGGL((dev::scoreI8Seg<NF, 1, false, dev::kSegTiles, true>), dim3(grid), dim3(256), 0, s, a,
+                hipLaunchKernelGGL((dev::scoreI8Seg<NF, 1, false, kSeg, true, W>), dim3(grid), dim3(64 * W), 0, s, a,
                                    a.mixTileOff, a.scores, nullptr, a.mixOddMask);
                 return;
             }
         }
-        // 16-tile segments for one K step (34 KiB per workgroup, 4 per CU); 8 for two (also 34 KiB)
-        hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS, false, (KS == 1 ? dev::kSegTiles : 8)>), dim3(grid), dim3(256),
-                           0, s, a, a.mixTileOff, a.scores, a.best, nullptr);
+        hipLaunchKernelGGL((dev::scoreI8Seg<NF, KS, false, kSeg, false, W>), dim3(grid), dim3(64 * W), 0, s, a,
+                           a.mixTileOff, a.scores, a.best, nullptr);
         return;
     }
 #endif
@@ -928,8 +932,12 @@ hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStr
         return hipErrorInvalidValue;
     if (a.smallTile && a.presel)
         return hipErrorInvalidValue;  // the preselection kernels keep their frame tile
-    // small calls: 64-frame waves (I8Args::smallTile)
-    if (kSteps == 1 && a.smallTile)
+    // small calls: 64-frame waves (I8Args::smallTile), one wave per workgroup for the smallest (2)
+    if (kSteps == 1 && a.smallTile == 2 && !multiCov)
+        launchI8T<4, 1, false, 1>(a, grid, stream);
+    else if (kSteps == 2 && a.smallTile == 2 && !multiCov)
+        launchI8T<4, 2, false, 1>(a, grid, stream);
+    else if (kSteps == 1 && a.smallTile)
         multiCov ? launchI8T<4, 1, true>(a, grid, stream) : launchI8T<4, 1, false>(a, grid, stream);
     else if (kSteps == 2 && a.smallTile)
         multiCov ? launchI8T<4, 2, true>(a, grid, stream) : launchI8T<4, 2, false>(a, grid, stream);
