@@ -53,6 +53,9 @@ constexpr int splitPreselNF(int ks) { return GMM_SPLIT_PRESEL_NF == 8 && ks <= 5
 #ifndef GMM_SPLIT_PF
 #define GMM_SPLIT_PF 2  // tile pairs in flight per wave (scoreSplit without preselection; 3: +2.6 % at D = 39, profiles/r04/s18)
 #endif
+#ifndef GMM_SPLIT_DIAG_HOT
+#define GMM_SPLIT_DIAG_HOT 0  // diagnostic (wrong results): every tile load reads the chunk's first two tiles (L1-hot)
+#endif
 #ifndef GMM_SPLIT_DIAG_NOEMIT
 #define GMM_SPLIT_DIAG_NOEMIT 0
 #endif
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
     const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS], uint2& Cw) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-            A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+            A[s] = th[(static_cast<size_t>(GMM_SPLIT_DIAG_HOT ? T0 + (tt & 1u) : tt) * KS + s) * 64 + lane];
         if constexpr (PRESEL)
             Cw = tclu[static_cast<size_t>(tt) * 4 + g];  // rows 4g .. 4g+3: cluster * 64, u16 each
     };
