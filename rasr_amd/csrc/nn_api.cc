@@ -7,12 +7,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/rasr_nn.h"
+#include "gmm_hostio.hh"
 #include "gmm_kernels.hh"  // launchTransposeWords (gmm_kernels_layout.hip)
 #include "nn_kernels.hh"
 
@@ -106,6 +108,19 @@ int collectTiming(nn_scorer* s) {
     s->nCalls += 1;
     s->pending = false;
     return GMM_OK;
+}
+
+}  // namespace
+
+namespace {
+
+// RASR_NN_SMALL_GEMM=0: calls of up to 64 frames on nnGemm8p as well (A/B)
+bool smallGemmEnabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RASR_NN_SMALL_GEMM");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 }  // namespace
@@ -227,7 +242,8 @@ int nn_score_device(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_
         return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frames/scores/stride");
     NN_HIP_CHECK(hipSetDevice(s->device));
     hipStream_t    st   = static_cast<hipStream_t>(stream);
-    const uint32_t Npad = roundUp(nFrames, kNnTileN);
+    const bool     small = nFrames <= kNnSmallFrames && smallGemmEnabled();
+    const uint32_t Npad  = small ? roundUp(nFrames, 16u) : roundUp(nFrames, kNnTileN);
     NN_HIP_CHECK(launchNnPrepareInput(frames, nFrames, frameStride, s->layers[0].K, s->layers[0].Kpad, s->dX0, st));
     if (s->timing) {
         int rc = collectTiming(s);
@@ -254,7 +270,7 @@ int nn_score_device(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_
         a.act         = L.act;
         a.gamma       = L.gamma;
         a.top         = top ? 1 : 0;
-        NN_HIP_CHECK(launchNnGemm(a, st));
+        NN_HIP_CHECK(small ? launchNnGemmSmall(a, st) : launchNnGemm(a, st));
         in = a.Y;
     }
     if (s->timing) {
@@ -295,15 +311,37 @@ int nn_score_host_ex(nn_scorer* s, const float* frames, uint32_t nFrames, uint32
         NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dHostT), static_cast<size_t>(s->maxFrames) * M * sizeof(float)));
     // only the caller's K used floats per frame row are read; only the call's rows / columns of a strided caller
     // table are written (the rest stays untouched, as with gmm_score_host)
+    // small calls (<= 64 frames) with page-locked buffers the device addresses at the same pointer: no copy engine,
+    // a kernel gathers the frame rows and the transpose / a strided copy kernel writes the caller's table over PCIe
+    // (as gmm_score_host_ring's small calls, gmm_api.cc scoreHostSmall)
+    static const bool smallOn = [] {  // RASR_GMM_SMALL_HOST=0: the copy-engine path (A/B)
+        const char* e = std::getenv("RASR_GMM_SMALL_HOST");
+        return !(e && e[0] == '0');
+    }();
+    const bool small =
+            smallOn && nFrames <= 64 && rasr_gmm::isDeviceMappedHost(frames) && rasr_gmm::isDeviceMappedHost(scores);
     int rc = GMM_OK;
     auto run = [&]() -> int {
-        NN_HIP_CHECK(hipMemcpy2DAsync(s->dHostF, static_cast<size_t>(K) * sizeof(float), frames,
-                                      static_cast<size_t>(frameStride) * sizeof(float), static_cast<size_t>(K) * sizeof(float),
-                                      nFrames, hipMemcpyHostToDevice, s->hostStream));
+        if (small)
+            NN_HIP_CHECK(rasr_gmm::launchCopyWords2D(reinterpret_cast<const uint32_t*>(frames), frameStride,
+                                                     reinterpret_cast<uint32_t*>(s->dHostF), K, nFrames, K, s->hostStream));
+        else
+            NN_HIP_CHECK(hipMemcpy2DAsync(s->dHostF, static_cast<size_t>(K) * sizeof(float), frames,
+                                          static_cast<size_t>(frameStride) * sizeof(float),
+                                          static_cast<size_t>(K) * sizeof(float), nFrames, hipMemcpyHostToDevice,
+                                          s->hostStream));
         int r = nn_score_device(s, s->dHostF, nFrames, K, s->dHostS, nFrames, s->hostStream);
         if (r != GMM_OK)
             return r;
-        if (frameMajor) {
+        if (small) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(s->dHostS);
+            uint32_t*       dst = reinterpret_cast<uint32_t*>(scores);
+            if (frameMajor)
+                NN_HIP_CHECK(rasr_gmm::launchTransposeWords(src, M, nFrames, nFrames, dst, scoreStride, s->hostStream));
+            else
+                NN_HIP_CHECK(rasr_gmm::launchCopyWords2D(src, nFrames, dst, scoreStride, M, nFrames, s->hostStream));
+        }
+        else if (frameMajor) {
             NN_HIP_CHECK(rasr_gmm::launchTransposeWords(reinterpret_cast<const uint32_t*>(s->dHostS), M, nFrames, nFrames,
                                                         reinterpret_cast<uint32_t*>(s->dHostT), M, s->hostStream));
             NN_HIP_CHECK(hipMemcpy2DAsync(scores, static_cast<size_t>(scoreStride) * sizeof(float), s->dHostT,

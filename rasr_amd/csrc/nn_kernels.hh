@@ -31,5 +31,8 @@ struct NnGemmArgs {
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
                                 uint32_t Kpad, uint16_t* X, hipStream_t stream);
 hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream);
+// calls of up to kNnSmallFrames frames (Npad = the frames rounded up to 16): one 16-unit row block per wave
+constexpr uint32_t kNnSmallFrames = 64;
+hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream);
 
 }  // namespace rasr_nn

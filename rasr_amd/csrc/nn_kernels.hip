@@ -337,7 +337,111 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// nnGemmSmall: calls of up to 64 frames (RASR's Nn::BatchFeatureScorer buffer-size defaults to 8,
+// src/Nn/BatchFeatureScorer.cc:21-22).  nnGemm8p's 256 x 256 tiles leave such a layer to Mpad / 256
+// workgroups (8 for 2048 units) that each sweep all of K: the call is latency-bound (~40 us per layer).
+// Here a workgroup owns 16 output units (one MFMA row block) x NB column blocks of 16 frames, its WS waves
+// split the K steps (Mpad / 16 workgroups per layer, 128 for 2048 units; 8 waves each: one round of KU = 8
+// K steps of loads per wave at K = 2048), every weight read once straight from HBM into the MFMA A fragment
+// (16 rows x 64 contiguous bytes per K step), the few frames' activations (<= 64 x Kpad bf16) from L2.  The
+// partial sums are added in wave order through LDS (deterministic), then nnGemm8p's epilogue: bias +
+// activation into the next layer's bf16 rows, or the negated scores of the top layer.
+// ---------------------------------------------------------------------------
+template <int NB, int WS>
+__global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
+    constexpr int KU = 8;  // K steps of 32 whose fragments are loaded ahead
+    __shared__ f32x4 part[WS][NB][64];
+    const int      lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t m0   = blockIdx.x * 16u;
+    const uint32_t rl = static_cast<uint32_t>(lane) & 15u, kq = 8u * (static_cast<uint32_t>(lane) >> 4);
+    // this wave's share of the K steps (Kpad / 32 of them, Kpad a multiple of 64)
+    const uint32_t nK = a.Kpad / 32u, per = (nK + WS - 1u) / WS;
+    const uint32_t k0 = min(nK, per * static_cast<uint32_t>(w)), k1 = min(nK, k0 + per);
+    const bf16x8*  wa = reinterpret_cast<const bf16x8*>(a.A + static_cast<size_t>(m0 + rl) * a.Kpad + kq);
+    const bf16x8*  xb[NB];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb)
+        xb[cb] = reinterpret_cast<const bf16x8*>(a.B + static_cast<size_t>(16u * cb + rl) * a.Kpad + kq);
+    f32x4 acc[NB];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb)
+        acc[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t k = k0;
+    for (; k + KU <= k1; k += KU) {
+        bf16x8 fa[KU], fb[KU][NB];
+#pragma unroll
+        for (int u = 0; u < KU; ++u) {
+            fa[u] = wa[(k + u) * 4u];  // 32 bf16 = four 16-byte pieces per K step
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb)
+                fb[u][cb] = xb[cb][(k + u) * 4u];
+        }
+#pragma unroll
+        for (int u = 0; u < KU; ++u)
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb)
+                acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u], fb[u][cb], acc[cb], 0, 0, 0);
+    }
+    for (; k < k1; ++k) {
+        const bf16x8 fa = wa[k * 4u];
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb)
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, xb[cb][k * 4u], acc[cb], 0, 0, 0);
+    }
+    // the WS partial sums, added in wave order (deterministic) by wave 0
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb)
+        part[w][cb][lane] = acc[cb];
+    __syncthreads();
+    if (w != 0)
+        return;
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+        acc[cb] = part[0][cb][lane];
+#pragma unroll
+        for (int v = 1; v < WS; ++v)
+            acc[cb] += part[v][cb][lane];
+    }
+    // accumulator r of lane l: unit m0 + 4 (l >> 4) + r, frame 16 cb + (l & 15)
+    const uint32_t mb = m0 + 4u * (static_cast<uint32_t>(lane) >> 4);
+    const f32x4    bs = *reinterpret_cast<const f32x4*>(a.bias + mb);
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+        const uint32_t n = 16u * cb + rl;
+        if (a.top) {
+            if (n < a.nFrames)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    if (mb + rr < a.M)
+                        a.scores[static_cast<size_t>(mb + rr) * a.scoreStride + n] = -(acc[cb][rr] + bs[rr]);
+        }
+        else {
+            u16x4 v;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                v[rr] = toBf16(activate(acc[cb][rr] + bs[rr], a.act, a.gamma));
+            *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
+        }
+    }
+}
+
 }  // namespace dev
+
+hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream) {
+    if (a.Mpad % 16u || a.Kpad % 64u || a.Kpad == 0 || a.Npad == 0 || a.Npad > 64 || a.Npad % 16u)
+        return hipErrorInvalidValue;
+    // one 16-unit row block per workgroup, its K steps split over kWs waves
+    constexpr int kWs = 8;
+    const dim3    grid(a.Mpad / 16u), block(64 * kWs);
+    switch (a.Npad / 16u) {
+        case 1: hipLaunchKernelGGL((dev::nnGemmSmall<1, kWs>), grid, block, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL((dev::nnGemmSmall<2, kWs>), grid, block, 0, stream, a); break;
+        case 3: hipLaunchKernelGGL((dev::nnGemmSmall<3, kWs>), grid, block, 0, stream, a); break;
+        default: hipLaunchKernelGGL((dev::nnGemmSmall<4, kWs>), grid, block, 0, stream, a); break;
+    }
+    return hipGetLastError();
+}
 
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
                                 uint32_t Kpad, uint16_t* X, hipStream_t stream) {

@@ -18,11 +18,31 @@ def main():
     ap.add_argument("--types", default="diagonal-maximum,SIMD-diagonal-maximum")
     ap.add_argument("--sizes", default="1,4,16,64")
     ap.add_argument("--calls", type=int, default=300)
+    ap.add_argument("--nn", action="store_true", help="the hybrid-DNN scorer instead of the GMM types")
     a = ap.parse_args()
     import rasr_amd as ra
     ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
     R = 64
     frames = ra.synthetic_frames(R, 39, seed=7)
+    if a.nn:  # the hybrid-DNN scorer's host call (bench.py NN_DIMS), frame-major into a page-locked table
+        from rasr_amd import nn
+        dims = [429] + [2048] * 6 + [5000]
+        sc = nn.NnScorer(nn.synthetic_network(dims, "sigmoid", seed=3), max_frames=R)
+        x = ra.pinned_empty((R, dims[0]))
+        x[:] = ra.synthetic_frames(R, dims[0], seed=9)
+        out = ra.pinned_empty((R, dims[-1]))
+        for n in (int(v) for v in a.sizes.split(",")):
+            for _ in range(10):
+                sc.score_host(x, out=out, n_frames=n, frame_major=True)
+            wall = []
+            for _ in range(a.calls // 3):
+                t0 = time.perf_counter()
+                sc.score_host(x, out=out, n_frames=n, frame_major=True)
+                wall.append(time.perf_counter() - t0)
+            med = statistics.median(wall) * 1e6
+            print(json.dumps({"type": "hybrid-dnn", "frames_per_call": n, "call_us_median": round(med, 1),
+                              "frames_per_s": round(n / (med * 1e-6), 1)}), flush=True)
+        return
     for kind in a.types.split(","):
         sc = ra.Scorer(ms, kind, max_frames=R)
         ring = ra.pinned_empty((R, 39))

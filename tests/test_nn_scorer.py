@@ -42,7 +42,10 @@ ACTS = ["sigmoid", "tanh", "relu", "elu", "identity"]
 @pytest.mark.gpu
 @pytest.mark.parametrize("act", ACTS)
 @pytest.mark.parametrize("dims,frames", [([39, 256, 100], 300), ([429, 1000, 1000, 997], 517),
-                                          ([45, 128, 128, 128, 64], 128), ([16, 5000], 33)])
+                                          ([45, 128, 128, 128, 64], 128), ([16, 5000], 33),
+                                          # <= 64 frames: nnGemmSmall (16-unit row blocks, 1..4 column blocks)
+                                          ([39, 256, 100], 1), ([45, 128, 128, 128, 64], 17),
+                                          ([429, 1000, 1000, 997], 64)])
 def test_nn_scorer_gpu(gpu, act, dims, frames):
     layers = nn.synthetic_network(dims, act, seed=len(dims) + frames)
     x = ra.synthetic_frames(frames, dims[0], seed=frames)
@@ -165,3 +168,29 @@ def test_nn_activations_near_zero(gpu, act):
         assert rel.max() <= 2 ** -6  # one bf16 ulp (<= 2^-7 relative) of the hidden output, either side, + series
     else:
         assert np.abs(s - ref).max() <= 1e-6 + 2 ** -7 * np.abs(ref).max()  # one bf16 ulp + exp(x) - 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frames", [1, 7, 64])
+@pytest.mark.parametrize("frame_major", [False, True])
+def test_nn_small_host_call_page_locked(gpu, frames, frame_major):
+    """nn_score_host_ex with page-locked frames and table (<= 64 frames: the one-stream path without the copy
+    engine) equals the pageable call bit for bit; the rest of a strided caller table stays untouched."""
+    layers = nn.synthetic_network([39, 256, 300], "sigmoid", seed=frames)
+    sc = nn.NnScorer(layers, max_frames=64)
+    x = ra.synthetic_frames(frames, 41, seed=frames + 3)  # row stride 41 > input 39
+    ref = sc.score_host(x, frame_major=frame_major)
+    xp = ra.pinned_empty(x.shape)
+    xp[:] = x
+    shape = (frames + 2, 300 + 5) if frame_major else (300, frames + 3)
+    out = ra.pinned_empty(shape)
+    out[:] = -3.0
+    sc.score_host(xp, out=out, frame_major=frame_major)
+    got = out[:frames, :300] if frame_major else out[:, :frames]
+    assert np.array_equal(np.ascontiguousarray(got).view(np.uint32), ref.view(np.uint32))
+    rest = np.ones(shape, bool)
+    if frame_major:
+        rest[:frames, :300] = False
+    else:
+        rest[:, :frames] = False
+    assert (out[rest] == -3.0).all()
