@@ -114,13 +114,13 @@ int collectTiming(nn_scorer* s) {
 
 namespace {
 
-// RASR_NN_SMALL_GEMM=0: calls of up to 64 frames on nnGemm8p as well (A/B)
-bool smallGemmEnabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("RASR_NN_SMALL_GEMM");
-        return !(e && e[0] == '0');
+// calls of up to this many frames run nnGemmSmall (RASR_NN_SMALL_FRAMES overrides, 0 = never: A/B)
+uint32_t smallGemmFrames() {
+    static const uint32_t n = [] {
+        const char* e = std::getenv("RASR_NN_SMALL_FRAMES");
+        return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : kNnSmallFrames;
     }();
-    return on;
+    return n;
 }
 
 }  // namespace
@@ -242,8 +242,8 @@ int nn_score_device(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_
         return fail(GMM_ERR_INVALID_ARGUMENT, "invalid frames/scores/stride");
     NN_HIP_CHECK(hipSetDevice(s->device));
     hipStream_t    st   = static_cast<hipStream_t>(stream);
-    const bool     small = nFrames <= kNnSmallFrames && smallGemmEnabled();
-    const uint32_t Npad  = small ? roundUp(nFrames, 16u) : roundUp(nFrames, kNnTileN);
+    const bool     small = nFrames <= smallGemmFrames();
+    const uint32_t Npad  = small ? roundUp(nFrames, nFrames <= 64 ? 16u : 64u) : roundUp(nFrames, kNnTileN);
     NN_HIP_CHECK(launchNnPrepareInput(frames, nFrames, frameStride, s->layers[0].K, s->layers[0].Kpad, s->dX0, st));
     if (s->timing) {
         int rc = collectTiming(s);

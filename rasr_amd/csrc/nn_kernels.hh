@@ -31,8 +31,12 @@ struct NnGemmArgs {
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
                                 uint32_t Kpad, uint16_t* X, hipStream_t stream);
 hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream);
-// calls of up to kNnSmallFrames frames (Npad = the frames rounded up to 16): one 16-unit row block per wave
-constexpr uint32_t kNnSmallFrames = 64;
+// calls of up to kNnSmallFrames frames (Npad = the frames rounded up to 16, beyond 64 to 64): one 16-unit row block
+// x <= 64 frames per workgroup (nnGemmSmall)
+#ifndef NN_SMALL_FRAMES
+#define NN_SMALL_FRAMES 256  // nnGemm8p from 512 frames on (profiles/r04/s28: 168 vs 278 us at 256, 309 vs 281 at 512)
+#endif
+constexpr uint32_t kNnSmallFrames = NN_SMALL_FRAMES;
 hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream);
 
 }  // namespace rasr_nn

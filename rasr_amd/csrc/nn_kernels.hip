@@ -353,7 +353,7 @@ __global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
     constexpr int KU = 8;  // K steps of 32 whose fragments are loaded ahead
     __shared__ f32x4 part[WS][NB][64];
     const int      lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t m0   = blockIdx.x * 16u;
+    const uint32_t m0   = blockIdx.x * 16u, n0 = blockIdx.y * 64u;  // 16 units x a group of <= 64 frames
     const uint32_t rl = static_cast<uint32_t>(lane) & 15u, kq = 8u * (static_cast<uint32_t>(lane) >> 4);
     // this wave's share of the K steps (Kpad / 32 of them, Kpad a multiple of 64)
     const uint32_t nK = a.Kpad / 32u, per = (nK + WS - 1u) / WS;
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
     const bf16x8*  xb[NB];
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb)
-        xb[cb] = reinterpret_cast<const bf16x8*>(a.B + static_cast<size_t>(16u * cb + rl) * a.Kpad + kq);
+        xb[cb] = reinterpret_cast<const bf16x8*>(a.B + static_cast<size_t>(n0 + 16u * cb + rl) * a.Kpad + kq);
     f32x4 acc[NB];
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb)
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
     const f32x4    bs = *reinterpret_cast<const f32x4*>(a.bias + mb);
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) {
-        const uint32_t n = 16u * cb + rl;
+        const uint32_t n = n0 + 16u * cb + rl;
         if (a.top) {
             if (n < a.nFrames)
 #pragma unroll
@@ -429,12 +429,13 @@ __global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
 }  // namespace dev
 
 hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream) {
-    if (a.Mpad % 16u || a.Kpad % 64u || a.Kpad == 0 || a.Npad == 0 || a.Npad > 64 || a.Npad % 16u)
+    // Npad: the frames rounded up to 16 (<= 64), or to 64 (groups of 64 frames, grid.y)
+    if (a.Mpad % 16u || a.Kpad % 64u || a.Kpad == 0 || a.Npad == 0 || a.Npad % 16u || (a.Npad > 64 && a.Npad % 64u))
         return hipErrorInvalidValue;
-    // one 16-unit row block per workgroup, its K steps split over kWs waves
+    // one 16-unit row block x frame group per workgroup, its K steps split over kWs waves
     constexpr int kWs = 8;
-    const dim3    grid(a.Mpad / 16u), block(64 * kWs);
-    switch (a.Npad / 16u) {
+    const dim3    grid(a.Mpad / 16u, (a.Npad + 63u) / 64u), block(64 * kWs);
+    switch (a.Npad > 64 ? 4u : a.Npad / 16u) {
         case 1: hipLaunchKernelGGL((dev::nnGemmSmall<1, kWs>), grid, block, 0, stream, a); break;
         case 2: hipLaunchKernelGGL((dev::nnGemmSmall<2, kWs>), grid, block, 0, stream, a); break;
         case 3: hipLaunchKernelGGL((dev::nnGemmSmall<3, kWs>), grid, block, 0, stream, a); break;

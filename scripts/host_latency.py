@@ -22,7 +22,7 @@ def main():
     a = ap.parse_args()
     import rasr_amd as ra
     ms = ra.synthetic_mixture_set(5000, 160, 39, seed=2024)
-    R = 64
+    R = max(64, max(int(v) for v in a.sizes.split(",")))
     frames = ra.synthetic_frames(R, 39, seed=7)
     if a.nn:  # the hybrid-DNN scorer's host call (bench.py NN_DIMS), frame-major into a page-locked table
         from rasr_amd import nn
@@ -34,13 +34,18 @@ def main():
         for n in (int(v) for v in a.sizes.split(",")):
             for _ in range(10):
                 sc.score_host(x, out=out, n_frames=n, frame_major=True)
+            sc.set_timing(True)
+            sc.kernel_time(reset=True)
             wall = []
             for _ in range(a.calls // 3):
                 t0 = time.perf_counter()
                 sc.score_host(x, out=out, n_frames=n, frame_major=True)
                 wall.append(time.perf_counter() - t0)
+            kms, launches = sc.kernel_time(reset=True)
+            sc.set_timing(False)
             med = statistics.median(wall) * 1e6
             print(json.dumps({"type": "hybrid-dnn", "frames_per_call": n, "call_us_median": round(med, 1),
+                              "layers_us": round(kms * 1e3 / max(launches, 1), 1),
                               "frames_per_s": round(n / (med * 1e-6), 1)}), flush=True)
         return
     for kind in a.types.split(","):
