@@ -123,6 +123,15 @@ uint32_t smallGemmFrames() {
     return n;
 }
 
+// layers whose nnGemm8p grid is smaller than this run nnGemm128 (RASR_NN_TILE128_WGS overrides, 0 = never: A/B)
+uint32_t tile128Wgs() {
+    static const uint32_t n = [] {
+        const char* e = std::getenv("RASR_NN_TILE128_WGS");
+        return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : kNnTile128Wgs;
+    }();
+    return n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -270,7 +279,11 @@ int nn_score_device(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_
         a.act         = L.act;
         a.gamma       = L.gamma;
         a.top         = top ? 1 : 0;
-        NN_HIP_CHECK(small ? launchNnGemmSmall(a, st) : launchNnGemm(a, st));
+        // the top layer keeps nnGemm8p from 2/3 of the limit on (its C^T form's 16-byte score stores; 2048 frames
+        // x 5000 classes, 160 tiles of 256: 194 vs 208 us for the whole network, profiles/r04/s30)
+        const uint32_t lim = top ? tile128Wgs() * 2u / 3u : tile128Wgs();
+        const bool     mid = !small && (L.Mpad / kNnTileM) * (Npad / kNnTileN) < lim;
+        NN_HIP_CHECK(small ? launchNnGemmSmall(a, st) : mid ? launchNnGemm128(a, st) : launchNnGemm(a, st));
         in = a.Y;
     }
     if (s->timing) {

@@ -34,9 +34,16 @@ hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream);
 // calls of up to kNnSmallFrames frames (Npad = the frames rounded up to 16, beyond 64 to 64): one 16-unit row block
 // x <= 64 frames per workgroup (nnGemmSmall)
 #ifndef NN_SMALL_FRAMES
-#define NN_SMALL_FRAMES 256  // nnGemm8p from 512 frames on (profiles/r04/s28: 168 vs 278 us at 256, 309 vs 281 at 512)
+#define NN_SMALL_FRAMES 192  // tile kernels beyond (profiles/r04/s30: 156 vs 158 us at 192, 166 vs 158 at 256)
 #endif
 constexpr uint32_t kNnSmallFrames = NN_SMALL_FRAMES;
 hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream);
+// layers whose nnGemm8p grid would have fewer than kNnTile128Wgs workgroups (Npad a multiple of 256): 128 x 128
+// tiles (nnGemm128), 4x the workgroups
+#ifndef NN_TILE128_WGS
+#define NN_TILE128_WGS 192  // profiles/r04/s30: 2048-unit layers on nnGemm128 up to 5888 frames
+#endif
+constexpr uint32_t kNnTile128Wgs = NN_TILE128_WGS;
+hipError_t launchNnGemm128(const NnGemmArgs& a, hipStream_t stream);
 
 }  // namespace rasr_nn

@@ -7,9 +7,10 @@
 // output tile per 512-thread workgroup on v_mfma_f32_16x16x32_bf16, K in 64-wide tiles staged global -> LDS
 // by global_load_lds_dwordx4, double-buffered, with counted s_waitcnt vmcnt and raw s_barriers (a
 // __syncthreads would drain the DMA).  Workgroups are mapped so that the ones sharing an XCD sweep the
-// output-unit tiles of one frame tile (its activations stay in that XCD's L2).  The variants measured
-// against it (a 128 x 128 tile, the two-half schedule, a persistent form, 32x32x16 quadrants, s_setprio
-// modes) are kept out of this file: scripts/variants/.
+// output-unit tiles of one frame tile (its activations stay in that XCD's L2).  Calls too small to fill the
+// chip with those tiles run nnGemm128 (128 x 128 tiles) or, up to 192 frames, nnGemmSmall.  The variants
+// measured against nnGemm8p (the two-half schedule, a persistent form, 32x32x16 quadrants, s_setprio modes;
+// DESIGN.md section 11) are kept out of this file: scripts/variants/.
 #include "gmm_kernels.hh"  // rasr_gmm::allowDynamicLds
 #include "nn_kernels.hh"
 
@@ -338,6 +339,111 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// nnGemm128: calls between nnGemmSmall's range and a full chip of nnGemm8p tiles (~300 .. 4000 frames).
+// There nnGemm8p's 256 x 256 tiles leave a 2048-unit layer Mpad / 256 x Npad / 256 workgroups (64 at 2048
+// frames): each sweeps all of K on one CU, so the layer takes one tile's time (~40 us) with most CUs idle.
+// A 128 x 128 tile gives 4x the workgroups for 1/4 of the work each.  256 threads as 2 x 2 waves of 64 x 64
+// (4 x 4 accumulators of v_mfma_f32_16x16x32_bf16); K in 64-wide stages staged global -> LDS by
+// global_load_lds_dwordx4 (4 x 1 KiB per wave and operand), double-buffered with a counted s_waitcnt vmcnt
+// and raw s_barriers; nnGemm8p's LDS swizzle and XCD mapping.  The K order of every accumulator chain and the
+// epilogue arithmetic are nnGemm8p's, so a frame's scores do not depend on which kernel a call size picks
+// (the top layer is not run as C^T here: 4-byte stores of 16 consecutive frames per class).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void nnGemm128(NnGemmArgs a) {
+    constexpr uint32_t T = 128, BK = 64, kOp = T * BK;
+    __shared__ __attribute__((aligned(16))) uint16_t lds[2][2][kOp];  // [stage][A | B], 64 KiB
+    const int      lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nMT = a.Mpad / T, nNT = a.Npad / T, nwg = nMT * nNT;
+    const uint32_t b = blockIdx.x, xcd = b & 7u, q = nwg / 8u, r = nwg % 8u;
+    const uint32_t id = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (b >> 3);
+    const uint32_t m0 = (id % nMT) * T, n0 = (id / nMT) * T;
+    const uint32_t wr = wave >> 1, wc = wave & 1u;
+    const uint32_t rl = static_cast<uint32_t>(lane) & 15u;
+
+    // stage s <- K columns [k0, k0 + 64): 16 pieces of 8 rows x 128 B per operand, 4 per wave
+    const auto issue = [&](uint32_t s, uint32_t k0) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t piece = wave * 4u + i;
+            const uint32_t row   = piece * 8u + (static_cast<uint32_t>(lane) >> 3);
+            const uint32_t c     = (static_cast<uint32_t>(lane) & 7u) ^ nnSwz(row);
+            __builtin_amdgcn_global_load_lds(a.A + static_cast<size_t>(m0 + row) * a.Kpad + k0 + 8u * c,
+                                             &lds[s][0][piece * 512u], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(a.B + static_cast<size_t>(n0 + row) * a.Kpad + k0 + 8u * c,
+                                             &lds[s][1][piece * 512u], 16, 0, 0);
+        }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    const uint32_t nK = a.Kpad / BK;
+    issue(0, 0);
+    for (uint32_t kt = 0; kt < nK; ++kt) {
+        const uint32_t s = kt & 1u;
+        if (kt + 1 < nK) {
+            issue(s ^ 1u, (kt + 1) * BK);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this stage's 8 DMAs landed, the next 8 fly
+        }
+        else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of stage s are in LDS
+#pragma unroll
+        for (uint32_t ks = 0; ks < 2; ++ks) {
+            bf16x8         fa[4], fb[4];
+            const uint32_t c = ks * 4u + (static_cast<uint32_t>(lane) >> 4);
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint32_t ra = wr * 64u + 16u * i + rl, rb = wc * 64u + 16u * i + rl;
+                fa[i] = *reinterpret_cast<const bf16x8*>(&lds[s][0][ra * BK + (c ^ nnSwz(ra)) * 8u]);
+                fb[i] = *reinterpret_cast<const bf16x8*>(&lds[s][1][rb * BK + (c ^ nnSwz(rb)) * 8u]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage s is free for the DMA of stage kt + 2
+    }
+
+    // epilogue: rows m = m0 + 64 wr + 16 i + 4 (lane >> 4) + rr, frame n = n0 + 64 wc + 16 j + (lane & 15)
+    const uint32_t g  = static_cast<uint32_t>(lane) >> 4;
+    const float    sk = -a.gamma * 1.44269504088896341f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t mb = m0 + wr * 64u + 16u * i + 4u * g;
+        const f32x4    bs = *reinterpret_cast<const f32x4*>(a.bias + mb);
+        const f32x4    bk = bs * sk;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t n = n0 + wc * 64u + 16u * j + rl;
+            if (a.top) {
+                if (n < a.nFrames)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        if (mb + rr < a.M)
+                            a.scores[static_cast<size_t>(mb + rr) * a.scoreStride + n] = -(acc[i][j][rr] + bs[rr]);
+                continue;
+            }
+            u16x4 v;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                v[rr] = a.act == 1  // nnGemm8p's sigmoid: bias and gamma folded into the exponent's FMA
+                            ? toBf16(__builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][rr], sk, bk[rr]))))
+                            : toBf16(activate(acc[i][j][rr] + bs[rr], a.act, a.gamma));
+            *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // nnGemmSmall: calls of up to 64 frames (RASR's Nn::BatchFeatureScorer buffer-size defaults to 8,
 // src/Nn/BatchFeatureScorer.cc:21-22).  nnGemm8p's 256 x 256 tiles leave such a layer to Mpad / 256
 // workgroups (8 for 2048 units) that each sweep all of K: the call is latency-bound (~40 us per layer).
@@ -441,6 +547,16 @@ hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream) {
         case 3: hipLaunchKernelGGL((dev::nnGemmSmall<3, kWs>), grid, block, 0, stream, a); break;
         default: hipLaunchKernelGGL((dev::nnGemmSmall<4, kWs>), grid, block, 0, stream, a); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launchNnGemm128(const NnGemmArgs& a, hipStream_t stream) {
+    if (a.Mpad % 128u || a.Npad % 128u || a.Kpad % kNnTileK || a.Kpad == 0 || a.swapped)
+        return hipErrorInvalidValue;  // whole tiles, no bounds checks
+    const uint32_t nwg = (a.Mpad / 128u) * (a.Npad / 128u);
+    if (nwg == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(dev::nnGemm128, dim3(nwg), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -45,7 +45,9 @@ ACTS = ["sigmoid", "tanh", "relu", "elu", "identity"]
                                           ([45, 128, 128, 128, 64], 128), ([16, 5000], 33),
                                           # <= 64 frames: nnGemmSmall (16-unit row blocks, 1..4 column blocks)
                                           ([39, 256, 100], 1), ([45, 128, 128, 128, 64], 17),
-                                          ([429, 1000, 1000, 997], 64)])
+                                          ([429, 1000, 1000, 997], 64),
+                                          # hidden layer on nnGemm8p (8 x 26 tiles of 256), top on nnGemm128
+                                          ([64, 2048, 300], 6400)])
 def test_nn_scorer_gpu(gpu, act, dims, frames):
     layers = nn.synthetic_network(dims, act, seed=len(dims) + frames)
     x = ra.synthetic_frames(frames, dims[0], seed=frames)
@@ -131,13 +133,16 @@ def test_nn_scorer_device_strides_and_errors(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("big", [False, True])
 @pytest.mark.parametrize("dims,frames", [([100, 70], 300),      # K 100 -> 2 K-tiles of 64
                                           ([150, 64, 33], 257),  # 3 K-tiles, then 4 (padded 256)
                                           ([64, 600, 10], 513),  # exactly 1 K-tile, then 12
                                           ([1, 5], 3)])          # a 1-wide input
-def test_nn_scorer_k_tile_counts(gpu, dims, frames):
-    # the GEMM's pipeline has separate paths for the last one and two K-tiles (no later stage to issue,
-    # s_waitcnt vmcnt(0) instead of the counted wait): every short K-tile count is exercised
+def test_nn_scorer_k_tile_counts(gpu, dims, frames, big):
+    # the GEMMs' pipelines have separate paths for the last one and two K-tiles (no later stage to issue,
+    # s_waitcnt vmcnt(0) instead of the counted wait): every short K-tile count is exercised, on nnGemm128
+    # (these layers' 256-tile grids are small) and, with 49152 more frames (>= 192 tiles of 256), on nnGemm8p
+    frames += 49152 if big else 0
     layers = nn.synthetic_network(dims, "tanh", seed=sum(dims))
     x = ra.synthetic_frames(frames, dims[0], seed=frames + 1)
     sc = nn.NnScorer(layers, max_frames=frames)
@@ -194,3 +199,18 @@ def test_nn_small_host_call_page_locked(gpu, frames, frame_major):
     else:
         rest[:, :frames] = False
     assert (out[rest] == -3.0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["sigmoid", "relu"])
+def test_nn_kernel_choice_bit_identical(gpu, act):
+    """A frame's scores do not depend on the call size's kernel: the first 1000 frames of a 6400-frame call
+    (every layer on nnGemm8p, 8 x 26 tiles of 256; top layer as C^T) equal a 1000-frame call of the same frames
+    (nnGemm128, 16 x 8 tiles of 128) bit for bit: same K order per accumulator chain, same epilogue arithmetic."""
+    layers = nn.synthetic_network([64, 2048, 2048], act, seed=21)
+    x = ra.synthetic_frames(6400, 64, seed=22)
+    sc = nn.NnScorer(layers, max_frames=6400)
+    full = sc.score_host(x)
+    part = sc.score_host(x[:1000])
+    assert np.array_equal(part.view(np.uint32), np.ascontiguousarray(full[:, :1000]).view(np.uint32))
+    assert _err(part, nn_oracle.forward_bf16(layers, x[:1000]).astype(np.float64)) <= 2e-3
