@@ -75,6 +75,7 @@ struct nn_scorer {
     float*             dHostF = nullptr;  // [maxFrames][K]
     float*             dHostS = nullptr;  // [M][maxFrames]
     float*             dHostT = nullptr;  // [maxFrames][M] (frame-major)
+    float*             dPart  = nullptr;  // nnGemm128 split-K partial sums [kNnSplitFloats]
 
     ~nn_scorer() {
         (void)hipSetDevice(device);
@@ -83,7 +84,7 @@ struct nn_scorer {
             (void)hipFree(l.dBias);
         }
         (void)hipFree(dX0);
-        for (float* p : {dHostF, dHostS, dHostT})
+        for (float* p : {dHostF, dHostS, dHostT, dPart})
             (void)hipFree(p);
         if (hostStream)
             (void)hipStreamDestroy(hostStream);
@@ -128,6 +129,25 @@ uint32_t tile128Wgs() {
     static const uint32_t n = [] {
         const char* e = std::getenv("RASR_NN_TILE128_WGS");
         return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : kNnTile128Wgs;
+    }();
+    return n;
+}
+
+// nnGemm128 splits the K range of hidden layers whose 128-tile grid is below kNnSplitWgs (RASR_NN_SPLIT_K=0: never)
+bool splitK() {
+    static const bool on = [] {
+        const char* e = std::getenv("RASR_NN_SPLIT_K");
+        return !e || std::strtoul(e, nullptr, 10) != 0;
+    }();
+    return on;
+}
+
+// the most workgroups a tile's K range is split over (RASR_NN_MAX_SPLIT overrides, 2..kNnMaxSplit: A/B)
+uint32_t maxSplit() {
+    static const uint32_t n = [] {
+        const char* e = std::getenv("RASR_NN_MAX_SPLIT");
+        const uint32_t v = e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 4u;
+        return std::max(2u, std::min(kNnMaxSplit, v));
     }();
     return n;
 }
@@ -219,6 +239,8 @@ int nn_scorer_create(const nn_network_desc* net, uint32_t maxFrames, int device,
     const size_t xBytes = static_cast<size_t>(s->maxFramesPad) * s->layers[0].Kpad * sizeof(uint16_t);
     NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dX0), xBytes));
     NN_HIP_CHECK(hipMemset(s->dX0, 0, xBytes));
+    if (splitK())
+        NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dPart), kNnSplitFloats * sizeof(float)));
     NN_HIP_CHECK(hipEventCreate(&s->ev0));
     NN_HIP_CHECK(hipEventCreate(&s->ev1));
     NN_HIP_CHECK(hipDeviceSynchronize());
@@ -283,6 +305,12 @@ int nn_score_device(nn_scorer* s, const float* frames, uint32_t nFrames, uint32_
         // x 5000 classes, 160 tiles of 256: 194 vs 208 us for the whole network, profiles/r04/s30)
         const uint32_t lim = top ? tile128Wgs() * 2u / 3u : tile128Wgs();
         const bool     mid = !small && (L.Mpad / kNnTileM) * (Npad / kNnTileN) < lim;
+        // hidden layers whose 128-tile grid leaves most CUs idle: K split over up to 4 workgroups per tile
+        const uint32_t wg128 = (L.Mpad / 128u) * (Npad / 128u);
+        if (mid && !top && s->dPart && wg128 < kNnSplitWgs) {
+            a.kSplit = std::min(maxSplit(), 2u * kNnSplitWgs / wg128);
+            a.part   = s->dPart;
+        }
         NN_HIP_CHECK(small ? launchNnGemmSmall(a, st) : mid ? launchNnGemm128(a, st) : launchNnGemm(a, st));
         in = a.Y;
     }

@@ -26,6 +26,10 @@ struct NnGemmArgs {
     float           gamma;
     int             top;
     int             swapped;   // top layer computed as C^T (A = activations, B = W^T): set by launchNnGemm
+    // nnGemm128 split-K (hidden layers of calls that leave most CUs idle): kSplit workgroups per tile sum K
+    // ranges into part [kSplit][Npad][Mpad] f32, nnSplitReduce adds them in split order + bias + activation
+    uint32_t        kSplit;    // 0 / 1: no split
+    float*          part;
 };
 
 hipError_t launchNnPrepareInput(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t D,
@@ -34,7 +38,7 @@ hipError_t launchNnGemm(const NnGemmArgs& a, hipStream_t stream);
 // calls of up to kNnSmallFrames frames (Npad = the frames rounded up to 16, beyond 64 to 64): one 16-unit row block
 // x <= 64 frames per workgroup (nnGemmSmall)
 #ifndef NN_SMALL_FRAMES
-#define NN_SMALL_FRAMES 192  // tile kernels beyond (profiles/r04/s30: 156 vs 158 us at 192, 166 vs 158 at 256)
+#define NN_SMALL_FRAMES 128  // split-K nnGemm128 beyond (profiles/r04/s32: 102 vs 117 us at 128, 155 vs 117 at 160)
 #endif
 constexpr uint32_t kNnSmallFrames = NN_SMALL_FRAMES;
 hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream);
@@ -45,5 +49,9 @@ hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream);
 #endif
 constexpr uint32_t kNnTile128Wgs = NN_TILE128_WGS;
 hipError_t launchNnGemm128(const NnGemmArgs& a, hipStream_t stream);
+// split-K workspace of a scorer: kSplit x Npad x Mpad f32 of a hidden layer split when its 128-tile grid is below
+// kNnSplitWgs, kSplit = min(kNnMaxSplit, 2 kNnSplitWgs / grid): <= 2 x kNnSplitWgs x 128 x 128 floats
+constexpr uint32_t kNnSplitWgs = 192, kNnMaxSplit = 8;
+constexpr size_t   kNnSplitFloats = static_cast<size_t>(2u * kNnSplitWgs) * 128u * 128u;
 
 }  // namespace rasr_nn

@@ -8,7 +8,7 @@
 // by global_load_lds_dwordx4, double-buffered, with counted s_waitcnt vmcnt and raw s_barriers (a
 // __syncthreads would drain the DMA).  Workgroups are mapped so that the ones sharing an XCD sweep the
 // output-unit tiles of one frame tile (its activations stay in that XCD's L2).  Calls too small to fill the
-// chip with those tiles run nnGemm128 (128 x 128 tiles) or, up to 192 frames, nnGemmSmall.  The variants
+// chip with those tiles run nnGemm128 (128 x 128 tiles) or, up to 128 frames, nnGemmSmall.  The variants
 // measured against nnGemm8p (the two-half schedule, a persistent form, 32x32x16 quadrants, s_setprio modes;
 // DESIGN.md section 11) are kept out of this file: scripts/variants/.
 #include "gmm_kernels.hh"  // rasr_gmm::allowDynamicLds
@@ -347,16 +347,20 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
 // global_load_lds_dwordx4 (4 x 1 KiB per wave and operand), double-buffered with a counted s_waitcnt vmcnt
 // and raw s_barriers; nnGemm8p's LDS swizzle and XCD mapping.  The K order of every accumulator chain and the
 // epilogue arithmetic are nnGemm8p's, so a frame's scores do not depend on which kernel a call size picks
-// (the top layer is not run as C^T here: 4-byte stores of 16 consecutive frames per class).
+// (the top layer is not run as C^T here: 4-byte stores of 16 consecutive frames per class).  A hidden layer whose
+// 128-tile grid still leaves CUs idle (kSplit > 1) splits K: workgroup idS covers tile idS % tiles over the
+// K-tiles of split idS / tiles and writes its f32 partial sums; nnSplitReduce finishes the layer.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void nnGemm128(NnGemmArgs a) {
     constexpr uint32_t T = 128, BK = 64, kOp = T * BK;
     __shared__ __attribute__((aligned(16))) uint16_t lds[2][2][kOp];  // [stage][A | B], 64 KiB
     const int      lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nMT = a.Mpad / T, nNT = a.Npad / T, nwg = nMT * nNT;
+    const uint32_t nMT = a.Mpad / T, nNT = a.Npad / T, nTiles = nMT * nNT;
+    const uint32_t S = a.kSplit > 1u ? a.kSplit : 1u, nwg = nTiles * S;
     const uint32_t b = blockIdx.x, xcd = b & 7u, q = nwg / 8u, r = nwg % 8u;
-    const uint32_t id = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (b >> 3);
+    const uint32_t idS = (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (b >> 3);
+    const uint32_t id = idS % nTiles, split = idS / nTiles;  // an XCD's workgroups: the tiles of one K range
     const uint32_t m0 = (id % nMT) * T, n0 = (id / nMT) * T;
     const uint32_t wr = wave >> 1, wc = wave & 1u;
     const uint32_t rl = static_cast<uint32_t>(lane) & 15u;
@@ -381,10 +385,13 @@ __global__ __launch_bounds__(256) void nnGemm128(NnGemmArgs a) {
         for (int j = 0; j < 4; ++j)
             acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    const uint32_t nK = a.Kpad / BK;
-    issue(0, 0);
-    for (uint32_t kt = 0; kt < nK; ++kt) {
-        const uint32_t s = kt & 1u;
+    // this workgroup's K-tiles [kt0, nK): all of K, or its split's share
+    const uint32_t nKall = a.Kpad / BK, per = (nKall + S - 1u) / S;
+    const uint32_t kt0 = min(nKall, split * per), nK = min(nKall, kt0 + per);
+    if (kt0 < nK)
+        issue(0, kt0 * BK);
+    for (uint32_t kt = kt0; kt < nK; ++kt) {
+        const uint32_t s = (kt - kt0) & 1u;
         if (kt + 1 < nK) {
             issue(s ^ 1u, (kt + 1) * BK);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this stage's 8 DMAs landed, the next 8 fly
@@ -415,6 +422,16 @@ __global__ __launch_bounds__(256) void nnGemm128(NnGemmArgs a) {
 
     // epilogue: rows m = m0 + 64 wr + 16 i + 4 (lane >> 4) + rr, frame n = n0 + 64 wc + 16 j + (lane & 15)
     const uint32_t g  = static_cast<uint32_t>(lane) >> 4;
+    if (S > 1u) {  // split K: the partial sums, 16 bytes of 4 units per frame; nnSplitReduce finishes the layer
+        float* const p = a.part + static_cast<size_t>(split) * a.Npad * a.Mpad;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<f32x4*>(p + static_cast<size_t>(n0 + wc * 64u + 16u * j + rl) * a.Mpad + m0 + wr * 64u +
+                                          16u * i + 4u * g) = acc[i][j];
+        return;
+    }
     const float    sk = -a.gamma * 1.44269504088896341f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -441,6 +458,28 @@ __global__ __launch_bounds__(256) void nnGemm128(NnGemmArgs a) {
             *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
         }
     }
+}
+
+// nnGemm128's split-K finish for a hidden layer: per frame n and 4 units m, the kSplit partial sums added in split
+// order (deterministic), then nnGemm8p's bias + activation epilogue into the next layer's bf16 rows
+__global__ __launch_bounds__(256) void nnSplitReduce(NnGemmArgs a) {
+    const uint32_t quads = a.Mpad / 4u;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= a.Npad * quads)
+        return;
+    const uint32_t n = t / quads, m = (t % quads) * 4u;
+    const size_t   off = static_cast<size_t>(n) * a.Mpad + m, plane = static_cast<size_t>(a.Npad) * a.Mpad;
+    f32x4          acc = *reinterpret_cast<const f32x4*>(a.part + off);
+    for (uint32_t s = 1; s < a.kSplit; ++s)
+        acc += *reinterpret_cast<const f32x4*>(a.part + s * plane + off);
+    const f32x4 bs = *reinterpret_cast<const f32x4*>(a.bias + m);
+    const float sk = -a.gamma * 1.44269504088896341f;
+    u16x4       v;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+        v[rr] = a.act == 1 ? toBf16(__builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(acc[rr], sk, bs[rr] * sk))))
+                           : toBf16(activate(acc[rr] + bs[rr], a.act, a.gamma));
+    *reinterpret_cast<u16x4*>(a.Y + off) = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -553,10 +592,18 @@ hipError_t launchNnGemmSmall(const NnGemmArgs& a, hipStream_t stream) {
 hipError_t launchNnGemm128(const NnGemmArgs& a, hipStream_t stream) {
     if (a.Mpad % 128u || a.Npad % 128u || a.Kpad % kNnTileK || a.Kpad == 0 || a.swapped)
         return hipErrorInvalidValue;  // whole tiles, no bounds checks
-    const uint32_t nwg = (a.Mpad / 128u) * (a.Npad / 128u);
+    const bool split = a.kSplit > 1u;
+    if (split && (a.top || !a.part || a.kSplit > kNnMaxSplit ||
+                  static_cast<size_t>(a.kSplit) * a.Npad * a.Mpad > kNnSplitFloats))
+        return hipErrorInvalidValue;  // hidden layers only, within the workspace
+    const uint32_t nwg = (a.Mpad / 128u) * (a.Npad / 128u) * (split ? a.kSplit : 1u);
     if (nwg == 0)
         return hipSuccess;
     hipLaunchKernelGGL(dev::nnGemm128, dim3(nwg), dim3(256), 0, stream, a);
+    if (split) {
+        const uint32_t n = a.Npad * (a.Mpad / 4u);
+        hipLaunchKernelGGL(dev::nnSplitReduce, dim3((n + 255u) / 256u), dim3(256), 0, stream, a);
+    }
     return hipGetLastError();
 }
 

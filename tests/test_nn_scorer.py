@@ -45,7 +45,7 @@ ACTS = ["sigmoid", "tanh", "relu", "elu", "identity"]
                                           ([45, 128, 128, 128, 64], 128), ([16, 5000], 33),
                                           # <= 64 frames: nnGemmSmall (16-unit row blocks, 1..4 column blocks)
                                           ([39, 256, 100], 1), ([45, 128, 128, 128, 64], 17),
-                                          ([429, 1000, 1000, 997], 64),
+                                          ([429, 1000, 1000, 997], 64), ([429, 1000, 1000, 997], 128),
                                           # hidden layer on nnGemm8p (8 x 26 tiles of 256), top on nnGemm128
                                           ([64, 2048, 300], 6400)])
 def test_nn_scorer_gpu(gpu, act, dims, frames):
@@ -204,13 +204,17 @@ def test_nn_small_host_call_page_locked(gpu, frames, frame_major):
 @pytest.mark.gpu
 @pytest.mark.parametrize("act", ["sigmoid", "relu"])
 def test_nn_kernel_choice_bit_identical(gpu, act):
-    """A frame's scores do not depend on the call size's kernel: the first 1000 frames of a 6400-frame call
-    (every layer on nnGemm8p, 8 x 26 tiles of 256; top layer as C^T) equal a 1000-frame call of the same frames
-    (nnGemm128, 16 x 8 tiles of 128) bit for bit: same K order per accumulator chain, same epilogue arithmetic."""
+    """A frame's scores do not depend on the call size's kernel: the first 1600 frames of a 6400-frame call
+    (every layer on nnGemm8p, 8 x 26 tiles of 256; top layer as C^T) equal a 1600-frame call of the same frames
+    (nnGemm128 without K split, 16 x 14 tiles of 128) bit for bit: same K order per accumulator chain, same
+    epilogue arithmetic.  Smaller calls split K (nnSplitReduce): their sums differ in rounding only."""
     layers = nn.synthetic_network([64, 2048, 2048], act, seed=21)
     x = ra.synthetic_frames(6400, 64, seed=22)
     sc = nn.NnScorer(layers, max_frames=6400)
     full = sc.score_host(x)
-    part = sc.score_host(x[:1000])
-    assert np.array_equal(part.view(np.uint32), np.ascontiguousarray(full[:, :1000]).view(np.uint32))
-    assert _err(part, nn_oracle.forward_bf16(layers, x[:1000]).astype(np.float64)) <= 2e-3
+    part = sc.score_host(x[:1600])
+    assert np.array_equal(part.view(np.uint32), np.ascontiguousarray(full[:, :1600]).view(np.uint32))
+    ref = nn_oracle.forward_bf16(layers, x[:500]).astype(np.float64)
+    assert _err(part[:, :500], ref) <= 2e-3
+    split = sc.score_host(x[:500])  # 16 x 4 tiles of 128, K split 4 ways
+    assert _err(split, ref) <= 2e-3
