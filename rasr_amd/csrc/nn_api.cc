@@ -239,7 +239,7 @@ int nn_scorer_create(const nn_network_desc* net, uint32_t maxFrames, int device,
     const size_t xBytes = static_cast<size_t>(s->maxFramesPad) * s->layers[0].Kpad * sizeof(uint16_t);
     NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dX0), xBytes));
     NN_HIP_CHECK(hipMemset(s->dX0, 0, xBytes));
-    if (splitK())
+    if (splitK() && maxFrames > smallGemmFrames())  // only calls beyond the small-call range split K
         NN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dPart), kNnSplitFloats * sizeof(float)));
     NN_HIP_CHECK(hipEventCreate(&s->ev0));
     NN_HIP_CHECK(hipEventCreate(&s->ev1));
