@@ -169,7 +169,7 @@ check-integration: integration/rasr/Mm/GpuFeatureScorer.cc integration/rasr/Mm/G
 HARNESS = $(BUILD)/tests/rasr_adapter_harness
 $(HARNESS): tests/rasr_harness/harness.cc tests/rasr_harness/gmm_standin.cc integration/rasr/Mm/GpuFeatureScorer.cc \
             integration/rasr/Mm/GpuFeatureScorer.hh $(SRC)/host/GpuFeatureScorer.cc $(SRC)/host/GpuFeatureScorer.hh \
-            $(wildcard tests/rasr_harness/include/*/*.hh) oracle
+            $(wildcard tests/rasr_harness/include/*/*.hh) | oracle
 	@mkdir -p $(BUILD)/tests
 	g++ -std=c++17 -O1 -Wall -Wno-unused-variable -Itests/rasr_harness/include -Iinclude -I$(SRC) -o $@ \
 	    tests/rasr_harness/harness.cc tests/rasr_harness/gmm_standin.cc integration/rasr/Mm/GpuFeatureScorer.cc \
@@ -199,7 +199,7 @@ check-integration-link: $(HARNESS) $(NN_HARNESS)
 # it); the oracle is linked as the checker.  Built here, run on the GPU by tests/test_integration.py (-m gpu).
 HARNESS_GPU = $(BUILD)/tests/rasr_adapter_harness_gpu
 $(HARNESS_GPU): tests/rasr_harness/harness.cc integration/rasr/Mm/GpuFeatureScorer.cc integration/rasr/Mm/GpuFeatureScorer.hh \
-                $(SRC)/host/GpuFeatureScorer.hh $(wildcard tests/rasr_harness/include/*/*.hh) $(LIB) oracle
+                $(SRC)/host/GpuFeatureScorer.hh $(wildcard tests/rasr_harness/include/*/*.hh) $(LIB) | oracle
 	@mkdir -p $(BUILD)/tests
 	g++ -std=c++17 -O1 -Wall -Wno-unused-variable -DHARNESS_PRODUCT -Itests/rasr_harness/include -Iinclude -I$(SRC) -o $@ \
 	    tests/rasr_harness/harness.cc integration/rasr/Mm/GpuFeatureScorer.cc \

@@ -43,9 +43,12 @@ import argparse
 import json
 import math
 import os
+import signal
 import socket
 import subprocess
 import sys
+import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -81,6 +84,12 @@ FRAMES_PER_LAUNCH = 32768  # frames per scorer call (the scorer's max_frames)
 DEFAULT_LAUNCHES = {"fp32": 12, "simd": 32, "bint": 40, "simd-scores": 40, "fp32-scores": 12, "sum": 8, "nn": 16, "presel-float": 8, "presel-int": 8}
 # BASELINE config 5 network (hybrid DNN): 11 x 39 spliced MFCC input, 6 sigmoid layers of 2048, 5000 classes
 NN_DIMS = [429] + [2048] * 6 + [5000]
+# N > 1 budget (the driver kills a run at 600 s): the headline and the other modes first (~1-2 min at N = 8), then
+# the checks of never-executed multi-GPU paths, each in child processes killed at FENCE_TIMEOUT_S; whatever still
+# runs at DEADLINE_S, the JSON line is printed with the extras that finished and every rank exits 0.
+FENCE_TIMEOUT_S = float(os.environ.get("RASR_BENCH_FENCE_TIMEOUT_S", 150))
+DEADLINE_S = 480.0
+PG_TIMEOUT_S = 180  # the ranks' process group: a collective that hangs aborts the rank instead of outliving the run
 
 
 def parse():
@@ -112,8 +121,14 @@ def parse():
     p.add_argument("--capi-sharded-child", default="",
                    help="internal: run the C-ABI density-sharded check over these comma-separated devices in this "
                         "process (started by rank 0 of an N > 1 run) and print one JSON record")
+    p.add_argument("--density-check-child", action="store_true",
+                   help="internal: one rank of the fenced density-sharded (config 4, RCCL) check, started by rank 0 "
+                        "of an N > 1 run; rank 0 of the check prints one JSON record")
     p.add_argument("--extras", choices=["auto", "off"], default="auto",
                    help="N = 1: device lines at 256/1024/4096 frames per call and the C++ drop-in protocol record")
+    p.add_argument("--deadline", type=float, default=float(os.environ.get("RASR_BENCH_DEADLINE_S", DEADLINE_S)),
+                   help="seconds after start at which the JSON line is printed with whatever extras have finished "
+                        "and every rank exits (0: no deadline)")
     return p.parse_args()
 
 
@@ -137,11 +152,31 @@ def launch_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def fence_probe() -> bool:
+    """RASR_BENCH_FENCE_PROBE=1 (tests/test_bench_fence.py, CPU): the N > 1 orchestration -- process group, fenced
+    children, deadline, the line -- with a synthetic headline and synthetic check payloads, no GPU work;
+    RASR_BENCH_INJECT=hang@R | raise@R | capi-hang | parent-hang@R injects a fault on rank R."""
+    return os.environ.get("RASR_BENCH_FENCE_PROBE") == "1"
+
+
+def _inject(what: str, rank: int) -> None:
+    """Probe mode only: RASR_BENCH_INJECT=<what>@<rank> (or <what> for every rank) raises ("raise") or hangs."""
+    spec = os.environ.get("RASR_BENCH_INJECT", "")
+    if not fence_probe() or not spec:
+        return
+    kind, _, r = spec.partition("@")
+    if kind == what and (r == "" or int(r) == rank):
+        if what == "raise":
+            raise RuntimeError(f"injected fault ({spec}) on rank {rank}")
+        while True:  # an injected hang: as a rank stuck in a collective whose peer never arrives
+            time.sleep(1)
+
+
 def dist_setup(args):
-    """One process per GPU over RCCL ("nccl").  Rehearsal only (not used by the driver): with
-    RASR_BENCH_SAME_DEVICE=1 every rank uses GPU 0 and RASR_BENCH_BACKEND=gloo replaces RCCL, so the
-    N > 1 flow can be exercised on a one-GPU box."""
-    import torch
+    """One process per GPU over RCCL ("nccl"), the process group with an explicit timeout (PG_TIMEOUT_S).
+    Rehearsal only (not used by the driver): with RASR_BENCH_SAME_DEVICE=1 every rank uses GPU 0 and
+    RASR_BENCH_BACKEND=gloo replaces RCCL, so the N > 1 flow can be exercised on a one-GPU box."""
+    import datetime
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -149,14 +184,21 @@ def dist_setup(args):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
     if os.environ.get("RASR_BENCH_SAME_DEVICE") == "1":
         local = 0
+    timeout = datetime.timedelta(seconds=PG_TIMEOUT_S)
+    if fence_probe():
+        if ws > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo", timeout=timeout)
+        return ws, rank, local
+    import torch
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         backend = os.environ.get("RASR_BENCH_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
         seen = dist.get_world_size()
         if seen != args.gpus:
             raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {seen} ranks")
@@ -711,40 +753,241 @@ def capi_sharded_child(args):
             "check": "bit-exact vs the unsharded scorer" if same else "MISMATCH vs the unsharded scorer"}
 
 
-def capi_sharded_check(args, ws, rank, timeout_s=300):
-    """N > 1 runs: rank 0 starts `bench.py --capi-sharded-child 0,...,N-1` as a child process (its own HIP
-    contexts and RCCL communicators; bounded by a timeout) while the other ranks wait on a gloo barrier (no
-    GPU work of theirs beside it).  Reported, never fatal to the headline."""
-    import torch
+# ---------------------------------------------------------------------------
+# N > 1: the checks of never-executed multi-GPU paths, fenced in child processes, and the run's deadline
+# ---------------------------------------------------------------------------
+_DIST_VARS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+              "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+              "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCH_NCCL_ASYNC_ERROR_HANDLING")
+
+
+def _kill_session(p) -> None:
+    """SIGKILL a fenced child and everything in its session (it was started with start_new_session)."""
+    try:
+        os.killpg(p.pid, signal.SIGKILL)
+    except (ProcessLookupError, PermissionError):
+        pass
+
+
+class LineGuard:
+    """The run's JSON line (rank 0), printed exactly once: by `emit()` at the end, or by the deadline watchdog with
+    the records that have finished (those still running marked as cut), after which every rank exits -- 0 once the
+    headline is measured.  Fenced children still running at the deadline are killed first."""
+
+    def __init__(self, rank: int, deadline_s: float):
+        self.rank, self.deadline_s = rank, deadline_s
+        self.line = None            # rank 0, once the headline is measured
+        self.headline_done = False  # every rank
+        self.pending = []           # records started, not finished
+        self.children = []          # fenced child processes
+        self._lock = threading.Lock()
+        self._printed = False
+        if deadline_s > 0:
+            t = threading.Timer(deadline_s, self._deadline)
+            t.daemon = True
+            t.start()
+
+    def begin(self, key: str) -> None:
+        with self._lock:
+            self.pending.append(key)
+
+    def set(self, key: str, value, sub: str | None = None) -> None:
+        """line[key] = value (or line[sub][key] = value)."""
+        with self._lock:
+            if key in self.pending:
+                self.pending.remove(key)
+            if self.line is not None:
+                (self.line[sub] if sub else self.line)[key] = value
+
+    def emit(self) -> None:
+        with self._lock:
+            if self._printed:
+                return
+            self._printed = True
+            if self.rank == 0 and self.line is not None:
+                print(json.dumps(self.line), flush=True)
+
+    def _deadline(self) -> None:
+        for p in list(self.children):
+            _kill_session(p)
+        with self._lock:
+            if not self._printed:
+                self._printed = True
+                if self.rank == 0 and self.line is not None:
+                    for k in self.pending:
+                        self.line[k] = {"error": f"still running at the {self.deadline_s:.0f} s deadline, cut"}
+                    self.line["deadline"] = {"seconds": self.deadline_s, "cut": list(self.pending)}
+                    print(json.dumps(self.line), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if self.headline_done else 3)
+
+
+def run_fenced(cmds, timeout_s: float, guard: LineGuard, grace_s: float = 10.0) -> dict:
+    """Run `cmds` ([(argv, env)], one per rank of a check) as child processes, each in its own session, and return
+    the last JSON line rank 0's child printed -- or an error record: the first child that exits non-zero (after
+    `grace_s` for the others to fail or finish) or the timeout kills every one of them, since a peer left inside a
+    collective would wait forever.  Never raises."""
+    procs, errs = [], []
+    t0 = time.monotonic()
+    try:
+        for argv, env in cmds:
+            out, err = tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")
+            p = subprocess.Popen(argv, env=env, stdout=out, stderr=err, stdin=subprocess.DEVNULL, text=True,
+                                 start_new_session=True)
+            procs.append((p, out, err))
+            guard.children.append(p)
+        failed_at, error = None, None
+        while True:
+            rcs = [p.poll() for p, _, _ in procs]
+            if all(rc is not None for rc in rcs):
+                break
+            now = time.monotonic()
+            if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+                failed_at = now
+            if failed_at is not None and now - failed_at > grace_s:
+                break
+            if now - t0 > timeout_s:
+                alive = [i for i, rc in enumerate(rcs) if rc is None]
+                error = f"timed out after {timeout_s:.0f} s (ranks still running: {alive}); killed"
+                break
+            time.sleep(0.2)
+        for p, _, _ in procs:
+            if p.poll() is None:
+                _kill_session(p)
+            p.wait()
+        texts = []
+        for p, out, err in procs:
+            out.seek(0)
+            err.seek(0)
+            texts.append((p.returncode, out.read(), err.read()))
+        bad = [(i, rc, e) for i, (rc, _, e) in enumerate(texts) if rc != 0]
+        if error is None and bad:
+            i, rc, e = bad[0]
+            error = f"rank {i} exited {rc}: {e.strip()[-300:]}"
+        if error is None:
+            lines = [x for x in texts[0][1].splitlines() if x.startswith("{")]
+            if not lines:
+                error = "no JSON record from rank 0"
+            else:
+                rec = json.loads(lines[-1])
+                rec["wall_s"] = round(time.monotonic() - t0, 1)
+                return rec
+        return {"error": error, "wall_s": round(time.monotonic() - t0, 1)}
+    except Exception as e:  # never fatal to the line
+        for p, _, _ in procs:
+            _kill_session(p)
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    finally:
+        for p, out, err in procs:
+            out.close()
+            err.close()
+            if p in guard.children:
+                guard.children.remove(p)
+
+
+def density_check_child(args):
+    """One rank of the fenced density-sharded check: its own process group (RCCL), the model, the check; rank 0
+    prints the record."""
     import torch.distributed as dist
-    rec = None
-    group = dist.new_group(backend="gloo")
+    ws, rank, local = dist_setup(args)
+    if fence_probe():
+        import torch
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        _inject("raise", rank)
+        _inject("hang", rank)
+        rec = {"scorer": "probe", "check": "probe", "ranks": ws, "sum": float(t.item())}
+    else:
+        import rasr_amd as ra
+        ms = ra.synthetic_mixture_set(args.mixtures, args.densities, args.dim, seed=2024)
+        rec = density_sharded_check(args, ms, ws, rank, local)
     if rank == 0:
-        n_vis = torch.cuda.device_count()
-        if n_vis < ws:
+        print(json.dumps(rec), flush=True)
+    dist.destroy_process_group()
+
+
+def fenced_extras(args, ws: int, rank: int, guard: LineGuard, group) -> None:
+    """Rank 0 runs, one after the other, (1) the density-sharded layout's check over RCCL as N fresh ranks of this
+    script (`--density-check-child`: their own process group, so a hang or a failure there cannot take the
+    headline's ranks with it) and (2) the C-ABI sharded handle over all GPUs in one child process
+    (`--capi-sharded-child`), each killed at FENCE_TIMEOUT_S; the other ranks wait on a gloo barrier.  The
+    records (or their errors) go into the line."""
+    import torch.distributed as dist
+    if rank == 0:
+        me = [sys.executable, os.path.abspath(__file__), "--mixtures", str(args.mixtures), "--densities",
+              str(args.densities), "--dim", str(args.dim), "--deadline", "0"]
+        env0 = {k: v for k, v in os.environ.items() if k not in _DIST_VARS}
+        env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        port = _free_port()
+        cmds = [(me + ["--gpus", str(ws), "--density-check-child"],
+                 dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(ws), LOCAL_WORLD_SIZE=str(ws),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))) for r in range(ws)]
+        guard.begin("density_sharded")
+        guard.set("density_sharded", run_fenced(cmds, FENCE_TIMEOUT_S, guard))
+        guard.begin("density_sharded_capi")
+        if fence_probe():
+            n_vis = ws
+        else:
+            import torch
+            n_vis = torch.cuda.device_count()
+        if n_vis < ws and os.environ.get("RASR_BENCH_SAME_DEVICE") != "1":
             rec = {"skipped": f"{n_vis} visible devices < {ws} ranks"}
         else:
-            env = {k: v for k, v in os.environ.items()
-                   if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
-                                "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
-            cmd = [sys.executable, os.path.abspath(__file__), "--capi-sharded-child",
-                   ",".join(str(d) for d in range(ws)), "--mixtures", str(args.mixtures), "--densities",
-                   str(args.densities), "--dim", str(args.dim)]
-            try:
-                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
-                last = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
-                rec = json.loads(last) if r.returncode == 0 and last.startswith("{") else {
-                    "error": f"child rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
-            except subprocess.TimeoutExpired:
-                rec = {"error": f"child timed out after {timeout_s} s"}
+            devs = ",".join("0" if os.environ.get("RASR_BENCH_SAME_DEVICE") == "1" else str(d) for d in range(ws))
+            rec = run_fenced([(me + ["--capi-sharded-child", devs], env0)], FENCE_TIMEOUT_S, guard)
+        guard.set("density_sharded_capi", rec)
     dist.barrier(group=group)
-    return rec
+
+
+def make_line(args, res, ws: int) -> dict:
+    n_dens = args.mixtures * args.densities
+    return {
+        "metric": "frames/sec scored, 39-dim x 800k-density diag-GMM",
+        "value": res["value"],
+        "unit": "frames/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": res["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "strong" if (args.parallel in ("mixtures", "densities") and ws > 1) else "weak",
+        "vs_baseline": None,
+        "dtype": res["dtype"],
+        "data": "synthetic (SURVEY 8(d): means N(0,1), var 0.5+|N(0,1)|, frames N(0,1))",
+        "config": {
+            "workload": f"{n_dens // 1000}k-density diag-GMM, {args.dim}-dim, {MODES[args.mode][0]}, "
+                        f"batched frames",
+            "scorer": MODES[args.mode][0],
+            "mixtures": args.mixtures,
+            "densities_per_mixture": "U[64, 256] (ragged, same total)" if args.ragged else args.densities,
+            "dimension": args.dim,
+            "frames_per_gpu_per_step": res["frames_per_step"],
+            "frames_per_launch": res["frames_per_launch"],
+            "best_density": not (args.no_best or args.mode.startswith("presel") or args.mode == "bint"
+                                 or args.mode.endswith("-scores")),
+            "parallelism": (f"mixture-sharded x{ws} + RCCL all-gather" if args.parallel == "mixtures" and ws > 1
+                            else f"density-sharded x{ws} + RCCL all-reduce(MIN) of split mixtures + all-gather"
+                            if args.parallel == "densities" and ws > 1 else f"frame-sharded replicas x{ws}"),
+        },
+        "timed_region_s": res["timed_region_s"],
+        "roofline": res["roofline"],
+        "cpu_baseline": None,
+        "host_boundary": None,
+    }
 
 
 def main():
     args = parse()
     if args.capi_sharded_child:
+        if fence_probe():
+            _inject("capi-hang", 0)
+            print(json.dumps({"probe": True, "devices": args.capi_sharded_child}), flush=True)
+            return
         print(json.dumps(capi_sharded_child(args)), flush=True)
+        return
+    if args.density_check_child:
+        density_check_child(args)
         return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
@@ -761,13 +1004,21 @@ def main():
         with open(os.path.join(os.environ["RASR_BENCH_LAUNCH_PROBE"], f"rank{rec['rank']}.json"), "w") as f:
             json.dump(rec, f)
         return
-    import rasr_amd as ra
+    probe = fence_probe()
     ws, rank, local = dist_setup(args)
+    guard = LineGuard(rank, args.deadline)
+    group = None
+    if ws > 1:
+        import datetime
+        import torch.distributed as dist
+        # the fenced phase's waiting room: gloo (host), outlasting both fenced children
+        group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=2 * FENCE_TIMEOUT_S + 120))
     launches = args.launches or DEFAULT_LAUNCHES[args.mode]
-    if args.mode == "nn":
+    if args.mode == "nn" and not probe:
         res = run_nn(args, ws, rank, local, launches)
+        guard.headline_done = True
         if rank == 0:
-            print(json.dumps({
+            guard.line = {
                 "metric": "frames/sec scored, hybrid-DNN posteriors (Nn::BatchFeatureScorer)", "value": res["value"],
                 "unit": "frames/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -776,93 +1027,56 @@ def main():
                            "frames_per_gpu_per_step": res["frames_per_step"],
                            "frames_per_launch": res["frames_per_launch"],
                            "parallelism": f"frame-sharded replicas x{ws}"},
-                "timed_region_s": res["timed_region_s"], "roofline": res["roofline"], "cpu_baseline": None}),
-                flush=True)
+                "timed_region_s": res["timed_region_s"], "roofline": res["roofline"], "cpu_baseline": None}
+        guard.emit()
         if ws > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
         return
-    counts = (ra.ragged_counts(args.mixtures, args.mixtures * args.densities) if args.ragged else args.densities)
-    ms = ra.synthetic_mixture_set(args.mixtures, counts, args.dim, seed=2024)
-    res = run_mode(args, args.mode, ms, ws, rank, local, launches)
-    extra = {}
-    if not args.no_extra_mode:
-        # the other headline-model scorers (nn returned above): fp32 / SIMD, and the batched int scorer
-        for other in [m for m in ("fp32", "simd", "bint", "simd-scores", "fp32-scores") if m != args.mode]:
-            r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_LAUNCHES[other])
-            extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
-                            "frames_per_gpu_per_step": r2["frames_per_step"],
-                            "frames_per_launch": r2["frames_per_launch"], "timed_region_s": r2["timed_region_s"],
-                            "dtype": r2["dtype"], "scorer": MODES[other][0], "roofline": r2["roofline"]}
-    dcheck = None
-    if ws > 1 and args.parallel == "frames" and args.mode in ("fp32", "simd") and not args.no_density_check:
-        dcheck = density_sharded_check(args, ms, ws, rank, local)
-    capi = None
-    if ws > 1 and args.parallel == "frames" and args.mode in ("fp32", "simd") and not args.no_density_check:
-        capi = capi_sharded_check(args, ws, rank)
-    cpu = None
-    hb = None
-    hb_all = None
-    batches = None
-    dropin = None
-    if rank == 0 and ws == 1 and args.host_boundary == "auto" and not args.mode.startswith("presel"):
-        hb = host_boundary(args, ms, MODES[args.mode][0])
-    if ws > 1 and args.host_boundary == "auto" and args.mode in ("fp32", "simd") and args.parallel == "frames":
-        hb_all = host_leg_all_ranks(args, ms, MODES[args.mode][0], ws, rank, local)
-    if rank == 0 and ws == 1 and args.extras == "auto" and args.mode in ("fp32", "simd"):
-        batches = {MODES[m][0]: small_batches(args, ms, MODES[m][0]) for m in ("fp32", "simd")}
-        dropin = {MODES[m][0]: drop_in(args, MODES[m][0]) for m in ("fp32", "simd")}
-    if rank == 0 and ws == 1 and args.cpu_baseline == "auto":
-        cpu = cpu_baseline(args, ms)
+    if probe:  # synthetic headline: the orchestration below is what is under test
+        ms = None
+        res = {"value": 1.0, "ms_per_step": 1.0, "dtype": "probe", "frames_per_step": 0, "frames_per_launch": 0,
+               "timed_region_s": 0.0, "roofline": None}
+    else:
+        import rasr_amd as ra
+        counts = (ra.ragged_counts(args.mixtures, args.mixtures * args.densities) if args.ragged else args.densities)
+        ms = ra.synthetic_mixture_set(args.mixtures, counts, args.dim, seed=2024)
+        res = run_mode(args, args.mode, ms, ws, rank, local, launches)
+    guard.headline_done = True
     if rank == 0:
-        n_dens = args.mixtures * args.densities
-        line = {
-            "metric": "frames/sec scored, 39-dim x 800k-density diag-GMM",
-            "value": res["value"],
-            "unit": "frames/s",
-            "n_gpus": ws,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": res["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": "strong" if (args.parallel in ("mixtures", "densities") and ws > 1) else "weak",
-            "vs_baseline": None,
-            "dtype": res["dtype"],
-            "data": "synthetic (SURVEY 8(d): means N(0,1), var 0.5+|N(0,1)|, frames N(0,1))",
-            "config": {
-                "workload": f"{n_dens // 1000}k-density diag-GMM, {args.dim}-dim, {MODES[args.mode][0]}, "
-                            f"batched frames",
-                "scorer": MODES[args.mode][0],
-                "mixtures": args.mixtures,
-                "densities_per_mixture": "U[64, 256] (ragged, same total)" if args.ragged else args.densities,
-                "dimension": args.dim,
-                "frames_per_gpu_per_step": res["frames_per_step"],
-                "frames_per_launch": res["frames_per_launch"],
-                "best_density": not (args.no_best or args.mode.startswith("presel") or args.mode == "bint"
-                                     or args.mode.endswith("-scores")),
-                "parallelism": (f"mixture-sharded x{ws} + RCCL all-gather" if args.parallel == "mixtures" and ws > 1
-                                else f"density-sharded x{ws} + RCCL all-reduce(MIN) of split mixtures + all-gather"
-                                if args.parallel == "densities" and ws > 1 else f"frame-sharded replicas x{ws}"),
-            },
-            "timed_region_s": res["timed_region_s"],
-            "roofline": res["roofline"],
-            "cpu_baseline": cpu,
-            "host_boundary": hb,
-        }
-        if hb_all is not None:
-            line["host_boundary_all_ranks"] = hb_all
-            line["config"]["process_group"] = {"backend": hb_all["backend"], "ranks": ws}
-        if batches is not None:
-            line["small_batches"] = batches
-        if dropin is not None:
-            line["drop_in_protocol"] = dropin
-        if extra:
-            line["modes"] = extra
-        if dcheck is not None:
-            line["density_sharded"] = dcheck
-        if capi is not None:
-            line["density_sharded_capi"] = capi
-        print(json.dumps(line), flush=True)
+        guard.line = make_line(args, res, ws)
+    multi = ws > 1 and args.parallel == "frames" and args.mode in ("fp32", "simd")
+    if not probe:
+        if not args.no_extra_mode:
+            # the other headline-model scorers (nn returned above): fp32 / SIMD, and the batched int scorer; the
+            # same collectives as the headline
+            extra = {}
+            for other in [m for m in ("fp32", "simd", "bint", "simd-scores", "fp32-scores") if m != args.mode]:
+                r2 = run_mode(args, other, ms, ws, rank, local, DEFAULT_LAUNCHES[other])
+                extra[other] = {"value": r2["value"], "ms_per_step": r2["ms_per_step"],
+                                "frames_per_gpu_per_step": r2["frames_per_step"],
+                                "frames_per_launch": r2["frames_per_launch"], "timed_region_s": r2["timed_region_s"],
+                                "dtype": r2["dtype"], "scorer": MODES[other][0], "roofline": r2["roofline"]}
+                guard.set("modes", dict(extra))
+        if rank == 0 and ws == 1 and args.host_boundary == "auto" and not args.mode.startswith("presel"):
+            guard.begin("host_boundary")
+            guard.set("host_boundary", host_boundary(args, ms, MODES[args.mode][0]))
+        if multi and args.host_boundary == "auto":
+            hb_all = host_leg_all_ranks(args, ms, MODES[args.mode][0], ws, rank, local)
+            guard.set("host_boundary_all_ranks", hb_all)
+            guard.set("process_group", {"backend": hb_all["backend"], "ranks": ws}, sub="config")
+        if rank == 0 and ws == 1 and args.extras == "auto" and args.mode in ("fp32", "simd"):
+            guard.begin("small_batches")
+            guard.set("small_batches", {MODES[m][0]: small_batches(args, ms, MODES[m][0]) for m in ("fp32", "simd")})
+            guard.begin("drop_in_protocol")
+            guard.set("drop_in_protocol", {MODES[m][0]: drop_in(args, MODES[m][0]) for m in ("fp32", "simd")})
+        if rank == 0 and ws == 1 and args.cpu_baseline == "auto":
+            guard.begin("cpu_baseline")
+            guard.set("cpu_baseline", cpu_baseline(args, ms))
+    if multi and not args.no_density_check:
+        _inject("parent-hang", rank)
+        fenced_extras(args, ws, rank, guard, group)
+    guard.emit()
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

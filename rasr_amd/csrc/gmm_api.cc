@@ -1461,14 +1461,18 @@ int gmm_scorer_create_sharded(const gmm_mixture_set* ms, gmm_scorer_type type, c
     std::unique_ptr<DensityGroup> g(new DensityGroup);
     g->split = splitMixtures(plan);
     g->lead  = devices[0];
-    // AUTO: RCCL when the parts span several GPUs, the on-device copy exchange when they share one
+    // AUTO: RCCL when the parts span several GPUs and librccl opens, else the copy exchange (it needs no library);
+    // only an explicit GMM_EXCHANGE_RCCL turns a missing RCCL into an error
     std::vector<int> gpus;
     for (uint32_t i = 0; i < nDevices; ++i)
         if (std::find(gpus.begin(), gpus.end(), devices[i]) == gpus.end())
             gpus.push_back(devices[i]);
-    g->exchange = g->split.empty() ? GMM_EXCHANGE_AUTO
-                                   : (exchange == GMM_EXCHANGE_AUTO ? (gpus.size() > 1 ? GMM_EXCHANGE_RCCL : GMM_EXCHANGE_COPY)
-                                                                    : exchange);
+    if (g->split.empty())
+        g->exchange = GMM_EXCHANGE_AUTO;
+    else if (exchange == GMM_EXCHANGE_AUTO)
+        g->exchange = (gpus.size() > 1 && rccl().error.empty()) ? GMM_EXCHANGE_RCCL : GMM_EXCHANGE_COPY;
+    else
+        g->exchange = exchange;
     if (g->exchange == GMM_EXCHANGE_RCCL && !rccl().error.empty())
         return fail(GMM_ERR_UNSUPPORTED, "the RCCL exchange: " + rccl().error);
     const size_t maxF = cfg.max_frames, nS = g->split.size();

@@ -346,8 +346,10 @@ __global__ __launch_bounds__(512) void nnGemm8p(NnGemmArgs a) {
 // (4 x 4 accumulators of v_mfma_f32_16x16x32_bf16); K in 64-wide stages staged global -> LDS by
 // global_load_lds_dwordx4 (4 x 1 KiB per wave and operand), double-buffered with a counted s_waitcnt vmcnt
 // and raw s_barriers; nnGemm8p's LDS swizzle and XCD mapping.  The K order of every accumulator chain and the
-// epilogue arithmetic are nnGemm8p's, so a frame's scores do not depend on which kernel a call size picks
-// (the top layer is not run as C^T here: 4-byte stores of 16 consecutive frames per class).  A hidden layer whose
+// epilogue arithmetic are nnGemm8p's, so WITHOUT a K split a frame's scores are bit-identical between the two
+// kernels (the top layer is not run as C^T here: 4-byte stores of 16 consecutive frames per class); a split layer
+// (nnSplitReduce) and nnGemmSmall (K over 8 waves) add partial sums in another order and round differently,
+// within the bf16 contract (tests/test_nn_scorer.py::test_nn_kernel_boundaries_within_contract).  A hidden layer whose
 // 128-tile grid still leaves CUs idle (kSplit > 1) splits K: workgroup idS covers tile idS % tiles over the
 // K-tiles of split idS / tiles and writes its f32 partial sums; nnSplitReduce finishes the layer.
 // ---------------------------------------------------------------------------
@@ -490,8 +492,9 @@ __global__ __launch_bounds__(256) void nnSplitReduce(NnGemmArgs a) {
 // split the K steps (Mpad / 16 workgroups per layer, 128 for 2048 units; 8 waves each: one round of KU = 8
 // K steps of loads per wave at K = 2048), every weight read once straight from HBM into the MFMA A fragment
 // (16 rows x 64 contiguous bytes per K step), the few frames' activations (<= 64 x Kpad bf16) from L2.  The
-// partial sums are added in wave order through LDS (deterministic), then nnGemm8p's epilogue: bias +
-// activation into the next layer's bf16 rows, or the negated scores of the top layer.
+// partial sums are added in wave order through LDS (deterministic; the K order differs from nnGemm8p's, so the
+// rounding does too), then nnGemm8p's epilogue arithmetic (the folded sigmoid included): bias + activation into
+// the next layer's bf16 rows, or the negated scores of the top layer.
 // ---------------------------------------------------------------------------
 template <int NB, int WS>
 __global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
@@ -551,6 +554,8 @@ __global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
     // accumulator r of lane l: unit m0 + 4 (l >> 4) + r, frame 16 cb + (l & 15)
     const uint32_t mb = m0 + 4u * (static_cast<uint32_t>(lane) >> 4);
     const f32x4    bs = *reinterpret_cast<const f32x4*>(a.bias + mb);
+    const float    sk = -a.gamma * 1.44269504088896341f;
+    const f32x4    bk = bs * sk;
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) {
         const uint32_t n = n0 + 16u * cb + rl;
@@ -565,7 +570,9 @@ __global__ __launch_bounds__(64 * WS) void nnGemmSmall(NnGemmArgs a) {
             u16x4 v;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr)
-                v[rr] = toBf16(activate(acc[cb][rr] + bs[rr], a.act, a.gamma));
+                v[rr] = a.act == 1  // nnGemm8p's sigmoid: bias and gamma folded into the exponent's FMA
+                            ? toBf16(__builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(acc[cb][rr], sk, bk[rr]))))
+                            : toBf16(activate(acc[cb][rr] + bs[rr], a.act, a.gamma));
             *reinterpret_cast<u16x4*>(a.Y + static_cast<size_t>(n) * a.Mpad + mb) = v;
         }
     }

@@ -46,8 +46,9 @@ ACTS = ["sigmoid", "tanh", "relu", "elu", "identity"]
                                           # <= 64 frames: nnGemmSmall (16-unit row blocks, 1..4 column blocks)
                                           ([39, 256, 100], 1), ([45, 128, 128, 128, 64], 17),
                                           ([429, 1000, 1000, 997], 64), ([429, 1000, 1000, 997], 128),
-                                          # hidden layer on nnGemm8p (8 x 26 tiles of 256), top on nnGemm128
-                                          ([64, 2048, 300], 6400)])
+                                          # hidden layer on nnGemm8p (Npad 8192: 8 x 32 = 256 tiles of 256, well
+                                          # above the 192-workgroup cutoff kNnTile128Wgs), top on nnGemm128
+                                          ([64, 2048, 300], 8192)])
 def test_nn_scorer_gpu(gpu, act, dims, frames):
     layers = nn.synthetic_network(dims, act, seed=len(dims) + frames)
     x = ra.synthetic_frames(frames, dims[0], seed=frames)
@@ -204,13 +205,14 @@ def test_nn_small_host_call_page_locked(gpu, frames, frame_major):
 @pytest.mark.gpu
 @pytest.mark.parametrize("act", ["sigmoid", "relu"])
 def test_nn_kernel_choice_bit_identical(gpu, act):
-    """A frame's scores do not depend on the call size's kernel: the first 1600 frames of a 6400-frame call
-    (every layer on nnGemm8p, 8 x 26 tiles of 256; top layer as C^T) equal a 1600-frame call of the same frames
-    (nnGemm128 without K split, 16 x 14 tiles of 128) bit for bit: same K order per accumulator chain, same
-    epilogue arithmetic.  Smaller calls split K (nnSplitReduce): their sums differ in rounding only."""
+    """Between nnGemm8p and UNSPLIT nnGemm128 a frame's scores do not depend on the call size: the first 1600
+    frames of an 8192-frame call (every layer on nnGemm8p, 8 x 32 = 256 tiles of 256, well above the
+    192-workgroup cutoff; top layer as C^T) equal a 1600-frame call of the same frames (nnGemm128 without K split,
+    16 x 14 tiles of 128) bit for bit: same K order per accumulator chain, same epilogue arithmetic.  Smaller
+    calls split K (nnSplitReduce) or run nnGemmSmall: their sums differ in rounding only."""
     layers = nn.synthetic_network([64, 2048, 2048], act, seed=21)
-    x = ra.synthetic_frames(6400, 64, seed=22)
-    sc = nn.NnScorer(layers, max_frames=6400)
+    x = ra.synthetic_frames(8192, 64, seed=22)
+    sc = nn.NnScorer(layers, max_frames=8192)
     full = sc.score_host(x)
     part = sc.score_host(x[:1600])
     assert np.array_equal(part.view(np.uint32), np.ascontiguousarray(full[:, :1600]).view(np.uint32))
@@ -218,3 +220,20 @@ def test_nn_kernel_choice_bit_identical(gpu, act):
     assert _err(part[:, :500], ref) <= 2e-3
     split = sc.score_host(x[:500])  # 16 x 4 tiles of 128, K split 4 ways
     assert _err(split, ref) <= 2e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["sigmoid", "tanh", "relu"])
+def test_nn_kernel_boundaries_within_contract(gpu, act):
+    """The same frames through each kernel the call size picks -- nnGemmSmall (<= 128 frames, K over 8 waves),
+    nnGemm128 with a K split (500 frames, nnSplitReduce), unsplit nnGemm128 (1600) and nnGemm8p (8192) -- agree
+    with each other within the bf16 contract (their partial sums are added in different orders, so they are not
+    bit-identical), and each with the oracle."""
+    layers = nn.synthetic_network([429, 2048, 2048, 1000], act, seed=31)
+    x = ra.synthetic_frames(8192, 429, seed=32)
+    sc = nn.NnScorer(layers, max_frames=8192)
+    calls = {n: sc.score_host(x[:n]) for n in (100, 500, 1600, 8192)}
+    ref = nn_oracle.forward_bf16(layers, x[:100]).astype(np.float64)
+    for n, s in calls.items():
+        assert _err(s[:, :100], ref) <= 2e-3, n
+        assert _err(s[:, :100], calls[100].astype(np.float64)) <= 4e-3, n
