@@ -153,11 +153,12 @@ struct gmm_scorer {
     DensityClustering       clustering;
     void*                   dClusterMeans = nullptr;
     uint32_t*               dSelT         = nullptr;  // [nFramesPad/64][clusters][16]
+    uint16_t*               dSelC         = nullptr;  // quantized: [nFramesPad/128][clusters][16] wave-table entries
     void*                   dTileClu      = nullptr;  // [tiles + pad][16]: u16 cluster * 64 (float), u32 cluster * 16 (int)
     uint32_t                lastFrames    = 0;
     // quantized scalars
     uint32_t idxBits = 1, paddedDimension = 0;
-    bool     scoreOnly   = false;    // class layout (batch types): no best densities, cheaper epilogue
+    int      scoreOnly   = kScoreOnlyNone;  // score-only layout (no best densities, cheaper epilogue): kScoreOnly*
     uint32_t* dMixOddMask = nullptr;
     float    scaling = 0, scalingSquared = 0, invQ = 0, batchScale = 0;
     std::vector<float>    isvScaled;     // [C][D] (quantized types)
@@ -224,7 +225,7 @@ struct gmm_scorer {
     ~gmm_scorer() {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
                         dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
-                        dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dTileClu, dCentre,
+                        dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dSelC, dTileClu, dCentre,
                         dDirMean, dDirConst, dDirLogNorm, dDirCov, dHostScoresT, dHostBestT, dMixOddMask};
         for (void* p : ptrs)
             if (p)
@@ -283,6 +284,8 @@ int selectClustersFor(gmm_scorer* s, const float* frames, uint32_t nFrames, uint
     GMM_HIP_CHECK(launchSelectClusters(s->quantized, frames, nFrames, frameStride, nPadCall, s->D,
                                        s->clustering.paddedDimension, s->dIsv, s->dClusterMeans,
                                        s->clustering.nClusters, s->clustering.nSelected, s->dSelT, stream));
+    if (s->dSelC)  // the quantized kernel's per-wave tables
+        GMM_HIP_CHECK(launchCompactSelection(s->dSelT, nPadCall, s->clustering.nClusters, s->dSelC, stream));
     s->lastFrames = nFrames;
     return GMM_OK;
 }
@@ -429,19 +432,22 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         a.idxBits     = s->idxBits;
         a.flavor      = s->flavor == Flavor::Simd ? 0 : 1;
         a.s2          = s->scalingSquared;
-        // SIMD finalize by multiplication (gmm_kernels_i8.hip, emitMixtureI8); scales far outside a real
-        // model's range keep the division
-        a.halfInvS2 = (s->scalingSquared >= 1e-30f && s->scalingSquared <= 1e30f)
-                              ? 0.5 * (1.0 / static_cast<double>(s->scalingSquared))
-                              : 0.0;
+        // finalize by multiplication and two corrections (gmm_kernels_i8.hip finalizeStoreI8): b = 2 s^2 (the SIMD
+        // scorer's 0.5 / s2, the batch scorers' scale_, both exactly 2 s2 in f32) and RN(1 / b) by IEEE division;
+        // scales far outside a real model's range keep the division
+        a.finB        = s->flavor == Flavor::Simd ? 2.0f * s->scalingSquared : s->batchScale;
+        a.finInv      = 1.0f / a.finB;
+        a.finInvLo    = static_cast<float>(1.0 / static_cast<double>(a.finB) - static_cast<double>(a.finInv));
+        a.finDivide   = (a.finB >= 1e-30f && a.finB <= 1e30f) ? 0 : 1;
         a.batchScale  = s->batchScale;
         a.outScale    = s->cfg.score_scale;
         a.presel      = s->presel ? 1 : 0;
         a.selT        = s->dSelT;
+        a.selC        = s->dSelC;
         a.tileClu     = s->dTileClu;
         a.nClusters   = s->clustering.nClusters;
         a.mixOddMask  = s->dMixOddMask;
-        a.scoreOnly   = s->scoreOnly ? 1 : 0;
+        a.scoreOnly   = s->scoreOnly;
         a.smallTile   = i8SmallTile(s, nFrames);
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
@@ -634,6 +640,11 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
     const size_t selBytes = static_cast<size_t>(s->nFramesPad / 64) * dc.nClusters * 64;
     GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dSelT), selBytes));
     GMM_HIP_CHECK(hipMemset(s->dSelT, 0xff, selBytes));
+    if (s->quantized && kI8PreselNF == 8) {
+        const size_t cBytes = static_cast<size_t>(s->nFramesPad / 128) * dc.nClusters * 16 * sizeof(uint16_t);
+        GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dSelC), cBytes));
+        GMM_HIP_CHECK(hipMemset(s->dSelC, 0, cBytes));
+    }
     return GMM_OK;
 }
 
@@ -1261,9 +1272,12 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
         PreparedQuantized p;
         // batch types have no best densities: the score-only class layout where it applies
         // (preselection-batch-int included: the kernel masks the class layout's candidates)
+        // (preselection-batch-int masks the class layout's candidates; the others run the slot layout)
         const bool        scoreOnlyLayout =
                 classLayout || (flavor == Flavor::BatchInt && !(cfg.flags & GMM_FLAG_FULL_KEYS));
-        std::string       err = prepareQuantized(*ms, flavor, shard, p, scoreOnlyLayout);
+        std::string       err = prepareQuantized(*ms, flavor, shard, p,
+                                                 !scoreOnlyLayout ? kScoreOnlyNone
+                                                                  : (presel ? kScoreOnlyClass : kScoreOnlySlots));
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
         s->scoreOnly = p.scoreOnly;

@@ -59,14 +59,18 @@ struct I8Args {
     uint32_t        idxBits;
     int             flavor;       // 0 SIMD-diagonal-maximum, 1 batch-int
     float           s2, batchScale, outScale;
-    double          halfInvS2;    // 0.5 * RN64(1 / s2) for the SIMD finalize, 0 = always divide (gmm_kernels_i8.hip)
+    float           finB, finInv; // the finalize's divisor b = 2 s^2 and RN(1 / b) (gmm_kernels_i8.hip finalizeStoreI8)
+    float           finInvLo;     // RN(1 / b - finInv): 1 / b as a sum of two floats
+    int             finDivide;    // 1: scales outside the range of the multiply-and-correct finalize, divide
     // preselection-batch-int (gmm_kernels_presel.hip): per-(frame, cluster) mask, per-row cluster offsets
     const uint32_t* selT;         // [nFramesPad/64][nClusters][16] u32, byte (frame%64)/16 = 0xff: deselected
+    const uint16_t* selC;         // [nFramesPad/128][nClusters][16] u16: the wave tables (launchCompactSelection)
     const void*     tileClu;      // u32 [T+pad][16]: cluster * 16 * kI8PreselEntryBytes (byte offset into a wave's table)
     uint32_t        nClusters;
     int             presel;
-    // score-only class layout (batch types, gmm_prepare.hh PreparedQuantized::scoreOnly): tileP is the
-    // MFMA's C input, mixOddMask[m] bit g = lane group g holds odd-Q rows
+    // score-only layouts (gmm_prepare.hh PreparedQuantized::scoreOnly): tileP is the MFMA's C input; 1 = the class
+    // layout (preselection-batch-int: mixOddMask[m] bit g = lane group g holds odd-Q rows, then mixed tiles), 2 = the
+    // slot layout (scoreI8Cls: mixOddMask[m] bit 2g + s = the rows of lane group g's register s hold odd-Q rows)
     const uint32_t* mixOddMask;
     int             scoreOnly;
     // small calls (no preselection): 1 = 64 frames per wave, 256 per workgroup (<= kI8SmallFrames frames: half
@@ -218,6 +222,9 @@ hipError_t launchSelectClusters(bool quantized, const float* frames, uint32_t nF
                                 uint32_t nFramesRead, uint32_t D, uint32_t Dp, const float* variance,
                                 const void* clusterMeans, uint32_t nClusters, uint32_t nSelected, uint32_t* selT,
                                 hipStream_t stream);
+// the quantized scorer's mask table: [nFramesRead / 128][nClusters][16] u16 entries from the byte mask
+hipError_t launchCompactSelection(const uint32_t* selT, uint32_t nFramesRead, uint32_t nClusters, uint16_t* selC,
+                                  hipStream_t stream);
 hipError_t launchScoreF32(const F32Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 
 }  // namespace rasr_gmm

@@ -109,21 +109,20 @@ __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restri
         const bool     none = MAYBE_NONE && packed == INT_MAX;
         const int      q    = none ? INT_MAX : (packed >> ib) + ssOut[i];
         const uint32_t dns  = none ? 0xffffffffu : static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
-        float score;
-        if (a.flavor == 0) {  // SimdFeatureScorer.cc:142: (f32)(0.5 * q / scalingSquared_) in double
-            // y = q * 0.5 RN64(1/s2) is within 3 ulp of the exact quotient, so (f32)y equals (f32) of the
-            // correctly rounded double quotient unless an f32 rounding midpoint (the 29 bits below f32
-            // precision = 2^28) lies within 4 ulp of y: then the division itself (never, in practice:
-            // tests/test_fastdiv_finalize.py)
-            const double   y  = static_cast<double>(q) * a.halfInvS2;
-            const uint32_t lo = static_cast<uint32_t>(__double_as_longlong(y)) & 0x1fffffffu;
-            if (a.halfInvS2 == 0.0 || lo - (0x10000000u - 4u) <= 8u)
-                score = static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2));
-            else
-                score = static_cast<float>(y);
-        }
-        else  // BatchFeatureScorer.cc:468: (f32)best / scale_
-            score = __fdiv_rn(static_cast<float>(q), a.batchScale);
+        // Both reference finalizes divide by b = 2 s^2: SimdFeatureScorer.cc:142 (f32)(0.5 * q / (f64)s2) and
+        // BatchFeatureScorer.cc:468 (f32)best / scale_ (scale_ = 2 s^2).  y = RN(x / b) from x (rh + rl) (1/b as two
+        // floats: within 2^-47 of x / b after one rounding, so a faithful quotient) and one Markstein correction
+        // (no special operands here: x a float integer, b a normal positive float).  batch: exactly the reference
+        // (x = (f32) best).  SIMD, |q| < 2^24: x = q; a quotient of two floats is never an f32 midpoint, and q / b
+        // is >= 2^-49 relative away from one, so the reference's double quotient (2^-53) rounds to the same f32.
+        // Larger |q| (never from a real mixture), and scales outside the range where this applies (finDivide),
+        // divide as the reference (tests/test_fastdiv_finalize.py: both in exact arithmetic).
+        const float x = static_cast<float>(q), b = a.finB, r = a.finInv;
+        const float y = __fmaf_rn(x, r, __fmul_rn(x, a.finInvLo));
+        float score   = __fmaf_rn(__fmaf_rn(-b, y, x), r, y);
+        if (a.finDivide != 0 || (a.flavor == 0 && static_cast<uint32_t>(q + (1 << 24)) >= (2u << 24)))
+            score = a.flavor == 0 ? static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2))
+                                  : __fdiv_rn(x, a.batchScale);
         // ScaledContextScorer::score (ScaledFeatureScorer.hh:62-64); a finite score times 1.0f is itself,
         // so the multiply is unconditional (a select on the uniform test costs more than the multiply)
         score = __fmul_rn(a.outScale, score);
@@ -459,6 +458,19 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
                                                             : (i >= kTileA / 4 + 16 ? neverClu : 0u);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before use by the first segment's barrier
     }
+    // preselection: this wave's mask table [cluster][16] after the segment ring
+    const uint32_t tabBase = 2 * kSegBytes + kDummyBytes;
+    const uint32_t words   = PRESEL ? a.nClusters * 16u : 0u;  // entries of a table (u32 words of a 64-frame block)
+    const uint32_t tabOff  = tabBase + static_cast<uint32_t>(wave) * (words + 16u) * kEntryBytes;
+    if constexpr (PRESEL && NF == 8) {
+        // the wave's 128 frames' table, built once per call (launchCompactSelection), by LDS-DMA ahead of the ring
+        // (the oldest vector-memory operations: the first segment's counted wait covers them)
+        const int8_t*  src   = reinterpret_cast<const int8_t*>(a.selC + static_cast<size_t>(frame0 / 128u) * words);
+        const uint32_t bytes = words * 2u;
+        for (uint32_t off = 0; off < bytes; off += 1024u)
+            if (off + static_cast<uint32_t>(lane) * 16u < bytes)
+                __builtin_amdgcn_global_load_lds(src + off + lane * 16, lds + tabOff + off, 16, 0, 0);
+    }
     if (nSeg > 0)
         issueSeg(0);
     if (nSeg > 1)
@@ -482,10 +494,8 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
     uint32_t laneSel = 0;  // byte offset of (wave table, column t = lane & 15)
     // compressed: per (cluster, t) the bits "frame 16 cb + t did not select the cluster" (bit cb), stored as the byte
     // offset of the entry of maskLut that expands them to one 0x00 / 0xff mask byte per column block (NF 4: 4 KiB
-    // per wave instead of 16, 5 workgroups per CU instead of 2)
-    const uint32_t tabBase = 2 * kSegBytes + kDummyBytes;
+    // per wave instead of 16, 5 workgroups per CU instead of 2).  NF 8: the table came by LDS-DMA (above)
     if constexpr (PRESEL) {
-        const uint32_t words = a.nClusters * 16u;  // u32 words of a 64-frame selection block (and table entries)
         for (uint32_t n = threadIdx.x; n < (NF == 8 ? 256u : 16u); n += 256u) {
             LutW v = 0;
 #pragma unroll
@@ -493,24 +503,14 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
                 v |= ((n >> cb) & 1u) ? LutW(0xff) << (8 * cb) : LutW(0);
             maskLut[n] = v;
         }
-        const uint32_t tabOff = tabBase + static_cast<uint32_t>(wave) * (words + 16u) * kEntryBytes;
-        // the selection words of this wave's frames: one 64-frame block (NF 4) or two (NF 8); bit 0 of byte q
-        // (0x00 / 0xff) of a word says frame 16 q + t of the block did not select the cluster
-        const i32x4* src0 = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
-        const i32x4* src1 = src0 + words / 4u;
-        const auto   nib  = [](uint32_t w) { return ((w & 0x01010101u) * 0x01020408u) >> 24 & 0xfu; };  // bit q = byte q
-        for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u) {
-            const i32x4 w0 = src0[i];
-            if constexpr (NF == 8) {
-                const i32x4 w1 = src1[i];
-                uint32_t    e[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j)  // entry: 8 * (bits of block 0 | bits of block 1 << 4)
-                    e[j] = (nib(static_cast<uint32_t>(w0[j])) | nib(static_cast<uint32_t>(w1[j])) << 4) * 8u;
-                reinterpret_cast<uint2*>(lds + tabOff)[i] = uint2{e[0] | e[1] << 16, e[2] | e[3] << 16};
-            }
-            else {
-                uint32_t packed = 0;
+        if constexpr (NF == 4) {
+            // the selection words of this wave's frames: one 64-frame block; bit 0 of byte q (0x00 / 0xff) of a
+            // word says frame 16 q + t of the block did not select the cluster
+            const i32x4* src0 = reinterpret_cast<const i32x4*>(a.selT + static_cast<size_t>(frame0 / 64u) * words);
+            const auto   nib  = [](uint32_t w) { return ((w & 0x01010101u) * 0x01020408u) >> 24 & 0xfu; };  // bit q = byte q
+            for (uint32_t i = static_cast<uint32_t>(lane); i < words / 4u; i += 64u) {
+                const i32x4 w0     = src0[i];
+                uint32_t    packed = 0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j)  // entry: 4 * the 4 bits
                     packed |= (nib(static_cast<uint32_t>(w0[j])) * 4u) << (8 * j);
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
         if (NF == 8 && lane >= 4 && lane < 8)
             reinterpret_cast<uint32_t*>(lds + tabOff + words * kEntryBytes)[lane] = 0x07f807f8u;
         laneSel = tabOff + (static_cast<uint32_t>(lane) & 15u) * kEntryBytes;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the table before the first segment's barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LUT and entries before the first segment's barrier
     }
     // a tile's row constants (the host biases them by 2^31 for PRESEL) and mask words of this lane's 4 rows,
     // from the tile's 64-byte row-constant block pRow and 64-byte cluster-offset block cRow
@@ -867,6 +867,270 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
     }
 }
 
+// ---------------------------------------------------------------------------
+// quantized scorer without best densities on the slot layout (gmm_prepare.cc buildSlotLayout): the SIMD
+// scorer's score-only twin, batch-diagonal-maximum-int / -fast.
+//
+// One tile per step: NF MFMAs with the tile's row constants h as the C input, so the accumulator holds
+// v = dot + h, and two v_min3 per MFMA into the lane's two running minima per column block (register s takes
+// rows s and s + 2 of the lane's four: one parity class of the mixture, bit 2g + s of its word).  Two v_min3 per
+// MFMA are exactly the vector-issue cycles an MFMA leaves free, so the step is otherwise bare: no mixed tiles, no
+// stand-in tile, no pack.  The epilogue of a step's last LAG column blocks runs in the next step under its first
+// MFMAs (no hazard wait at a step end); the first step of the next mixture completes the previous one that way and
+// emits it -- 2 min(v) + p per register, the reduce, finalize, stores -- under its own MFMAs, then its candidates
+// set the minima (no resets).  Tiles come through scoreI8Seg's LDS ring (LDS-DMA one segment ahead); each step reads
+// the next tile's operands from LDS.
+// ---------------------------------------------------------------------------
+#ifndef GMM_I8_CLS_LAG
+#define GMM_I8_CLS_LAG 3  // column blocks whose epilogue runs one step late
+#endif
+#ifndef GMM_I8_CLS_DIAG
+#define GMM_I8_CLS_DIAG 0  // timing diagnostics only (wrong results): 1 = no per-mixture emit (the last one aside)
+#endif
+template <int NF, int SEG, int W>
+__global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, const uint32_t* __restrict__ mixTileOff,
+                                                                    float* __restrict__ scores,
+                                                                    const uint32_t* __restrict__ mixWord) {
+    static_assert(NF == 4 || NF == 8, "NF");
+    constexpr int      LAG       = GMM_I8_CLS_LAG;
+    constexpr int      NPL       = NF / 4;
+    constexpr uint32_t kSegA     = SEG * 1024u;
+    constexpr uint32_t kSegBytes = kSegA + SEG * 64u;
+    constexpr int      kPieces   = SEG / W;          // 1 KiB operand pieces per wave per segment
+    constexpr uint32_t kRowLanes = 4u * SEG / W;     // lanes loading 16 B of row constants per wave
+    constexpr int      kIssued   = kPieces + 1;
+    constexpr int      kNeutral  = 0x3fffffff;       // above every row (padding rows: 0x30000000)
+    static_assert(SEG % W == 0 && kRowLanes <= 64 && LAG >= 1 && LAG < NF, "segment / lag");
+    // + 64: the look-ahead read past the last tile of buffer 1 stays inside the array
+    __shared__ __attribute__((aligned(16))) int8_t lds[2 * kSegBytes + 64];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int g    = lane >> 4;
+    uint32_t  chunk, ft;
+    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
+        return;  // uniform over the workgroup, before any barrier
+    const uint32_t frame0 = ft * (W * NF * 16u) + static_cast<uint32_t>(wave) * (NF * 16u);
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
+    const uint32_t nSeg = (T1 - T0 + SEG - 1) / SEG;
+    const int8_t*  gA   = static_cast<const int8_t*>(a.tileA);
+    const int8_t*  gP   = static_cast<const int8_t*>(a.tileP);
+
+    const auto issueSeg = [&](uint32_t s) {  // tile arrays are padded by kTilePad >= SEG tiles
+        const uint32_t t0   = T0 + s * SEG;
+        int8_t*        base = lds + (s & 1u) * kSegBytes;
+#pragma unroll
+        for (int i = 0; i < kPieces; ++i) {
+            const uint32_t piece = static_cast<uint32_t>(wave * kPieces + i);
+            __builtin_amdgcn_global_load_lds(gA + static_cast<size_t>(t0) * 1024u + piece * 1024u + lane * 16,
+                                             base + piece * 1024u, 16, 0, 0);
+        }
+        if (lane < kRowLanes)
+            __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * (kRowLanes * 16) + lane * 16,
+                                             base + kSegA + wave * (kRowLanes * 16), 16, 0, 0);
+    };
+    if (nSeg > 0)
+        issueSeg(0);
+    if (nSeg > 1)
+        issueSeg(1);
+
+    i32x4 B[NF];
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb)
+        B[cb] = reinterpret_cast<const i32x4*>(a.frameQ + static_cast<size_t>(frame0 + cb * 16 + (lane & 15)) * 64)[g];
+    int ssOut[NPL];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i)
+        ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
+
+    // mixture m ends at tile tEnd; its word wCur and the next mixture's end tNext are loaded one mixture ahead
+    // (scalar loads whose latency the mixture's steps cover)
+    uint32_t m = m0, tEnd = mixTileOff[m0 + 1], tNext = m0 + 1 < m1 ? mixTileOff[m0 + 2] : T1, wCur = mixWord[m0];
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    i32x2 best[NF];  // the lane's two running minima per column block (a register pair: 64-bit resets)
+    i32x4 acc[NF];   // acc[NF - LAG ..]: the previous step's blocks whose epilogue is pending
+    const uint64_t kNeutral2 = (static_cast<uint64_t>(kNeutral) << 32) | static_cast<uint32_t>(kNeutral);
+    // one v_min3 per two candidates; the empty asm keeps each update one v_min3 (the compiler would reassociate
+    // the chain into two-operand v_min), the min itself stays compiler-visible (hazard wait states)
+    const auto epiMin = [&](int cb) {
+        int b0 = min(best[cb][0], min(acc[cb][0], acc[cb][2]));
+        int b1 = min(best[cb][1], min(acc[cb][1], acc[cb][3]));
+        asm volatile("" : "+v"(b0));
+        asm volatile("" : "+v"(b1));
+        best[cb] = i32x2{b0, b1};
+    };
+    const auto epiSet = [&](int cb) {  // a mixture's first tile: the minima start from its candidates
+        best[cb] = i32x2{min(acc[cb][0], acc[cb][2]), min(acc[cb][1], acc[cb][3])};
+    };
+    // per-mixture emit: 2 min(v) + p per register (p = bit 2g + s of the word), the lane's two registers merged,
+    // the reduce-scatter over the lane groups, finalize and store
+    const auto emit = [&](uint32_t mm) {
+        const uint32_t w = wCur;
+        int            v[NF][1];
+        if (((w ^ (w >> 1)) & 0x55u) == 0u) {  // both registers of every lane group share the parity (uniform)
+            const int p = static_cast<int>((w >> (2 * g)) & 1u);
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                v[cb][0] = static_cast<int>((static_cast<uint32_t>(min(best[cb][0], best[cb][1])) << 1) + p);
+        }
+        else {
+            const int p0 = static_cast<int>((w >> (2 * g)) & 1u), p1 = static_cast<int>((w >> (2 * g + 1)) & 1u);
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                v[cb][0] = min(static_cast<int>((static_cast<uint32_t>(best[cb][0]) << 1) + p0),
+                               static_cast<int>((static_cast<uint32_t>(best[cb][1]) << 1) + p1));
+        }
+        emitMixtureI8<NF, false, 1>(a, scores, nullptr, v, mm, frame0, lane, g, 0, ssOut);
+    };
+    const auto emitNone = [&](uint32_t mm) {  // a mixture without densities: Core::Type<int>::max
+        int none[NF][1];
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+            none[cb][0] = INT_MAX;
+        emitMixtureI8<NF, true, 1>(a, scores, nullptr, none, mm, frame0, lane, g, 0, ssOut);
+    };
+    const auto advance = [&]() {  // m -> m + 1
+        ++m;
+        tEnd = tNext;
+        if (m < m1) {
+            wCur  = mixWord[m];
+            tNext = m + 1 < m1 ? mixTileOff[m + 2] : T1;
+        }
+    };
+    // mixture m ended at tile t: emit it (and the mixtures without tiles that end at t too)
+    const auto finish = [&](uint32_t t) {
+        if (!(GMM_I8_CLS_DIAG & 1) || m + 1 == m1)
+            emit(m);
+        advance();
+        while (t == tEnd && m < m1) {
+            emitNone(m);
+            advance();
+        }
+    };
+    // the step of one tile: MFMA of block cb beside the epilogue of block cb - LAG (of the previous step for cb <
+    // LAG), fenced so the scheduler keeps that pairing.  FIRST: the first tile of a mixture (after boundary()): no
+    // pending tail; its candidates set the minima of its first NF - LAG blocks (no reset of those)
+    const auto step = [&](const i32x4& A, const i32x4& P, uint32_t t, auto firstC) {
+        constexpr bool kFirst = decltype(firstC)::value;
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            __builtin_amdgcn_sched_barrier(0);
+            acc[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[cb], P, 0, 0, 0);
+            if (cb >= LAG) {
+                if (kFirst)
+                    epiSet(cb - LAG);
+                else
+                    epiMin(cb - LAG);
+            }
+            else if (!kFirst)
+                epiMin(NF - LAG + cb);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 64, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // mixture m ends at tile t and another with tiles follows: the pending tail completes m, which is emitted; the
+    // tail's minima restart above every row (the next mixture's first step sets the others)
+    const auto boundary = [&](uint32_t t) {
+#pragma unroll
+        for (int cb = NF - LAG; cb < NF; ++cb)
+            epiMin(cb);
+        finish(t);
+#pragma unroll
+        for (int cb = NF - LAG; cb < NF; ++cb)
+            asm volatile("v_mov_b64 %0, %1" : "=v"(best[cb]) : "s"(kNeutral2));
+    };
+    const std::true_type  kFirstTile{};
+    const std::false_type kInner{};
+    // before the chunk's first tile: minima above every row, and a pending tail that changes nothing
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb)
+        asm volatile("v_mov_b64 %0, %1" : "=v"(best[cb]) : "s"(kNeutral2));
+#pragma unroll
+    for (int cb = NF - LAG; cb < NF; ++cb)
+        acc[cb] = i32x4{kNeutral, kNeutral, kNeutral, kNeutral};
+    while (m < m1 && tEnd == T0) {  // mixtures without tiles at the start of the chunk
+        emitNone(m);
+        advance();
+    }
+    bool fresh = false;  // the next step is the first of a mixture (its minima not yet started)
+
+    for (uint32_t s = 0; s < nSeg; ++s) {
+        // this segment's pieces (issued one segment ago) have landed; the next segment's stay in flight
+        if (s + 1 < nSeg)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kIssued) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const int8_t*  base   = lds + (s & 1u) * kSegBytes;
+        const uint32_t segT0  = T0 + s * SEG;
+        const uint32_t segEnd = min(segT0 + SEG, T1);
+        // this lane's operand addresses of the current tile t; tile t + i is i KiB (A) and i * 64 B (P) further
+        const int8_t* pa = base + lane * 16;
+        const int8_t* pp = base + kSegA + g * 16;
+        const auto    rd = [&](int i, i32x4& A, i32x4& P) {  // (past the segment: read, never used)
+            A = *reinterpret_cast<const i32x4*>(pa + i * 1024);
+            P = *reinterpret_cast<const i32x4*>(pp + i * 64);
+        };
+        i32x4    A0, P0, A1, P1;  // tile t, and the next one in flight
+        uint32_t t = segT0;
+        rd(0, A0, P0);
+        while (t < segEnd) {
+            if (fresh) {  // the first tile of a mixture
+                rd(1, A1, P1);
+                step(A0, P0, t, kFirstTile);
+                A0 = A1;
+                P0 = P1;
+                pa += 1024;
+                pp += 64;
+                ++t;
+                fresh = false;
+            }
+            const uint32_t mEnd = min(segEnd, tEnd);
+            // two tiles per iteration on alternating registers (no copies of the operands in flight)
+            for (; t + 2 <= mEnd; t += 2) {
+                rd(1, A1, P1);
+                step(A0, P0, t, kInner);
+                rd(2, A0, P0);
+                step(A1, P1, t + 1, kInner);
+                pa += 2048;
+                pp += 128;
+            }
+            if (t < mEnd) {
+                rd(1, A1, P1);
+                step(A0, P0, t, kInner);
+                A0 = A1;
+                P0 = P1;
+                pa += 1024;
+                pp += 64;
+                ++t;
+            }
+            if (t == tEnd && t < T1) {  // mixture m ends here and another with tiles follows
+                boundary(t);
+                fresh = true;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (s & 1)
+        if (s + 2 < nSeg)
+            issueSeg(s + 2);
+    }
+    // the chunk's last mixture with tiles (its pending tail first), then trailing mixtures without tiles
+    if (m < m1) {
+#pragma unroll
+        for (int cb = NF - LAG; cb < NF; ++cb)
+            epiMin(cb);
+        emit(m);
+        advance();
+        while (m < m1) {
+            emitNone(m);
+            advance();
+        }
+    }
+}
+
 }  // namespace dev
 
 using dev::prepareFramesI8;
@@ -908,7 +1172,12 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
         // workgroups take half of that (more of them per CU)
         constexpr int kSeg = (KS == 1 ? dev::kSegTiles : 8) / (W == 1 ? 2 : 1);
         if constexpr (KS == 1) {
-            if (a.scoreOnly) {  // batch types on the class layout
+            if (a.scoreOnly == 2) {  // calls without best densities on the slot layout
+                hipLaunchKernelGGL((dev::scoreI8Cls<NF, kSeg, W>), dim3(grid), dim3(64 * W), 0, s, a, a.mixTileOff,
+                                   a.scores, a.mixOddMask);
+                return;
+            }
+            if (a.scoreOnly) {  // the class layout
                 hipLaunchKernelGGL((dev::scoreI8Seg<NF, 1, false, kSeg, true, W>), dim3(grid), dim3(64 * W), 0, s, a,
                                    a.mixTileOff, a.scores, nullptr, a.mixOddMask);
                 return;
@@ -926,7 +1195,8 @@ hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStr
     const uint32_t grid = 8u * ((a.nChunks + 7u) / 8u) * a.nFrameTiles;
     if (grid == 0)
         return hipSuccess;
-    if (a.presel && (multiCov || !GMM_I8_LDS || a.nClusters == 0 || a.nClusters > 256 || !a.selT || !a.tileClu))
+    if (a.presel && (multiCov || !GMM_I8_LDS || a.nClusters == 0 || a.nClusters > 256 || !a.selT || !a.tileClu ||
+                     (kI8PreselNF == 8 && !a.selC)))
         return hipErrorInvalidValue;
     if (a.scoreOnly && (multiCov || kSteps != 1 || !GMM_I8_LDS || !a.mixOddMask))
         return hipErrorInvalidValue;

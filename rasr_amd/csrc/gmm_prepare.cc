@@ -303,12 +303,94 @@ static std::string buildClassLayout(const gmm_mixture_set& ms, ShardRange shard,
         t.mixTileOffset[mi + 1] = t.nTiles;
     }
     out.idxBits   = 0;
-    out.scoreOnly = true;
+    out.scoreOnly = kScoreOnlyClass;
+    return "";
+}
+
+// Slot layout (kScoreOnlySlots: calls without best densities, preselection aside).  The 16 rows of a tile form 8
+// classes (g, s) -- rows 4g + s and 4g + s + 2, the rows that lane group g's running-minimum register s collects
+// in scoreI8Cls.  Every tile of a mixture gives class (g, s) the same parity of Q = c + sum a'^2 (bit 2g + s of the
+// mixture word: odd), so the kernel keeps min(v = dot + h) per register, one v_min3 per two candidates in every
+// tile, and forms 2 v + p once, at the mixture end.  With e even classes (the classes 0 .. e-1 in the order 2g + s)
+// a tile holds 2e even and 2(8 - e) odd rows; T is the smallest tile count that holds the mixture's nE even and nO
+// odd rows, e an even number where one fits (both registers of a lane group then share the parity: the kernel's
+// cheaper emit).  No mixed tiles: in exchange for their per-candidate 2 v + p, a mixture may need one tile more
+// (11 instead of 10 at 160 densities).  Unused rows carry kClassPadC and zero operands.
+static std::string buildSlotLayout(const gmm_mixture_set& ms, ShardRange shard, PreparedQuantized& out) {
+    const uint32_t D = out.dimension, Dp = out.paddedDimension, nMix = shard.end - shard.begin;
+    Tiling&        t = out.tiling;
+    t                = Tiling();
+    t.mixTileOffset.assign(nMix + 1, 0);
+    out.mixOddMask.assign(nMix, 0);
+    out.tileA.clear();
+    out.tileP.clear();
+    std::vector<uint32_t> cls[2];
+    std::vector<int64_t>  qOf;
+    for (uint32_t mi = 0; mi < nMix; ++mi) {
+        const uint32_t m = shard.begin + mi;
+        const uint32_t b = ms.mixture_offsets[m], e = ms.mixture_offsets[m + 1];
+        t.maxEntriesPerMixture = std::max(t.maxEntriesPerMixture, e - b);
+        cls[0].clear();
+        cls[1].clear();
+        qOf.assign(e - b, 0);
+        for (uint32_t x = b; x < e; ++x) {
+            const uint8_t* pm    = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
+            int64_t        sumSq = 0;
+            for (uint32_t k = 0; k < D; ++k) {
+                const int64_t an = 128 - static_cast<int32_t>(pm[k]);
+                sumSq += an * an;
+            }
+            qOf[x - b] = static_cast<int64_t>(out.constantWeight[x]) + sumSq;
+            cls[static_cast<uint64_t>(qOf[x - b]) & 1u].push_back(x);
+        }
+        const uint32_t nE = static_cast<uint32_t>(cls[0].size()), nO = static_cast<uint32_t>(cls[1].size());
+        uint32_t       T = (nE + nO + 15) / 16, ev = 0;
+        for (;; ++T) {  // smallest T, then an even e if one fits
+            int pick = -1;
+            for (uint32_t c = 0; c <= 8; ++c)
+                if (2 * c * T >= nE && 2 * (8 - c) * T >= nO && (pick < 0 || (pick & 1)))
+                    pick = static_cast<int>(c);
+            if (pick >= 0 || nE + nO == 0) {
+                ev = pick < 0 ? 8 : static_cast<uint32_t>(pick);
+                break;
+            }
+        }
+        out.mixOddMask[mi] = (0xffu << ev) & 0xffu;
+        const uint32_t t0 = t.nTiles;
+        t.nTiles += T;
+        out.tileA.resize(static_cast<size_t>(t.nTiles) * kLanes * 16, 0);
+        out.tileP.resize(static_cast<size_t>(t.nTiles) * kTileRows, kClassPadC);
+        t.rowEntry.resize(static_cast<size_t>(t.nTiles) * kTileRows, UINT32_MAX);
+        t.rowDensityInMixture.resize(static_cast<size_t>(t.nTiles) * kTileRows, UINT32_MAX);
+        t.tileCovariance.resize(t.nTiles, 0);
+        for (int p = 0; p < 2; ++p) {
+            const uint32_t c0 = p ? ev : 0, nc = p ? 8 - ev : ev;  // the classes of this parity
+            for (size_t i = 0; i < cls[p].size(); ++i) {
+                const uint32_t x = cls[p][i];
+                // tile by tile: the class's 2 rows, class after class
+                const uint32_t tile = t0 + static_cast<uint32_t>(i / (2 * nc));
+                const uint32_t c = c0 + static_cast<uint32_t>(i % (2 * nc)) / 2, j = static_cast<uint32_t>(i % 2);
+                const uint32_t r = 4 * (c >> 1) + (c & 1) + 2 * j;  // row 4g + s + 2j
+                const uint8_t* pm = out.preparedMean.data() + static_cast<size_t>(x) * Dp;
+                for (uint32_t kk = 0; kk < D; ++kk) {
+                    const int32_t  an   = 128 - static_cast<int32_t>(pm[kk]);
+                    const uint32_t lane = (kk / 16) * 16 + r, jj = kk % 16;  // one K step: kk < 64
+                    out.tileA[(static_cast<size_t>(tile) * kLanes + lane) * 16 + jj] = static_cast<int8_t>(an);
+                }
+                out.tileP[static_cast<size_t>(tile) * kTileRows + r]            = static_cast<int32_t>(qOf[x - b] >> 1);
+                t.rowEntry[static_cast<size_t>(tile) * kTileRows + r]            = x;
+                t.rowDensityInMixture[static_cast<size_t>(tile) * kTileRows + r] = x - b;
+            }
+        }
+        t.mixTileOffset[mi + 1] = t.nTiles;
+    }
+    out.idxBits   = 0;
+    out.scoreOnly = kScoreOnlySlots;
     return "";
 }
 
 std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out,
-                             bool scoreOnlyLayout) {
+                             int scoreOnlyLayout) {
     std::string err = validate(ms);
     if (!err.empty())
         return err;
@@ -397,10 +479,10 @@ std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRang
         for (uint32_t k = 0; k < D; ++k)
             out.isvDevice[static_cast<size_t>(c) * out.kSteps * kI8K + k] = out.isvScaled[static_cast<size_t>(c) * D + k];
     // a mixture whose plan does not fit the mixture word keeps the whole model on the key layout
-    if (scoreOnlyLayout && C == 1 && out.kSteps == 1 && classLayoutFits(ms, shard, out) &&
-        buildClassLayout(ms, shard, out).empty())
+    if (scoreOnlyLayout != kScoreOnlyNone && C == 1 && out.kSteps == 1 && classLayoutFits(ms, shard, out) &&
+        (scoreOnlyLayout == kScoreOnlySlots ? buildSlotLayout(ms, shard, out) : buildClassLayout(ms, shard, out)).empty())
         return "";
-    out.scoreOnly = false;
+    out.scoreOnly = kScoreOnlyNone;
     out.mixOddMask.clear();
 
     // device tiles

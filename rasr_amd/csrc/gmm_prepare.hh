@@ -62,6 +62,9 @@ struct Tiling {
     uint32_t              maxEntriesPerMixture = 0;
 };
 
+// score-only layouts of the quantized scorers (PreparedQuantized::scoreOnly, I8Args::scoreOnly)
+constexpr int kScoreOnlyNone = 0, kScoreOnlyClass = 1, kScoreOnlySlots = 2;
+
 struct PreparedQuantized {
     Flavor   flavor = Flavor::Simd;
     uint32_t dimension = 0, paddedDimension = 0, nCovariances = 0, nMixtures = 0;
@@ -83,8 +86,11 @@ struct PreparedQuantized {
     // groups (bit g of mixOddMask[m]: lane group g holds odd-Q rows); its mixed tiles that follow hold the
     // rest, evens first in row order (gmm_prepare.cc buildClassLayout, gmm_kernels_i8.hip SCORE_ONLY).
     // mixOddMask[m]: bits 0-3 the odd lane groups, bits 4-15 the first odd index of the mixed rows, bits
-    // 16-31 the class tile count.
-    bool                 scoreOnly = false;
+    // 16-31 the class tile count.  That is kScoreOnlyClass, the layout preselection-batch-int masks.
+    // kScoreOnlySlots (the other calls without best densities; gmm_prepare.cc buildSlotLayout,
+    // gmm_kernels_i8.hip scoreI8Cls): no mixed tiles; every tile gives the 8 classes (g, s) -- rows 4g + s and
+    // 4g + s + 2 -- the parity of bit 2g + s of mixOddMask[m].
+    int                  scoreOnly = 0;   // kScoreOnlyNone / kScoreOnlyClass / kScoreOnlySlots
     std::vector<uint32_t> mixOddMask;  // [nMixtures]
 };
 
@@ -140,9 +146,10 @@ struct PreparedDirect {
 
 // Returns empty string on success, else an error message.
 std::string validate(const gmm_mixture_set& ms);
-// scoreOnlyLayout: lay out the class layout above when it applies (out.scoreOnly says whether it did)
+// scoreOnlyLayout: lay out that score-only layout (kScoreOnlyClass / kScoreOnlySlots) when it applies (out.scoreOnly
+// says whether it did)
 std::string prepareQuantized(const gmm_mixture_set& ms, Flavor flavor, ShardRange shard, PreparedQuantized& out,
-                             bool scoreOnlyLayout = false);
+                             int scoreOnlyLayout = kScoreOnlyNone);
 // wantSplit: lay the model out for the split-f16 kernel when it applies (one covariance,
 // 3*dimension+7 <= 256, row constants below 2^30); out.split says whether it did.
 std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixtureWeightScale, float gaussianScale,

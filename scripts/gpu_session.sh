@@ -9,6 +9,8 @@
 #   ab-MODE : scripts/ab_bench.py --mode MODE over AB_LIBS (default: the variant libraries), AB_ARGS appended
 #   pmc-MODE: scripts/profile_pmc.sh MODE (one rocprofv3 --pmc pass per counter group, gpurun_out/pmc_MODE)
 #   line-X  : one other bench line, timed alone (X: sum sums d45 d45s pint pfloat nn ragged)
+#   rehearse: the N > 1 bench flow on this one GPU (2 ranks on device 0, gloo in place of RCCL): headline, the
+#             fenced density-sharded / C-ABI children, the line
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${RUN:-session}
 mkdir -p "$OUT"
@@ -31,6 +33,8 @@ for s in ${STEPS:-pytest smoke}; do
     prof)   step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py ${BENCH_ARGS} ;;
     ab-*)   step "$s" 900 python scripts/ab_bench.py --mode "${s#ab-}" ${AB_ARGS} ${AB_LIBS:-rasr_amd/lib/variants/*.so} ;;
     pmc-*)  step "$s" 1000 bash scripts/profile_pmc.sh "${s#pmc-}" ;;
+    rehearse) RASR_BENCH_SAME_DEVICE=1 RASR_BENCH_BACKEND=gloo step rehearse 420 python bench.py --gpus 2 --steps 3 \
+                --warmup 1 --no-extra-mode --host-boundary off ;;
     line-*)
       B="--gpus 1 --steps 20 --warmup 3 --cpu-baseline off --host-boundary off --extras off --no-extra-mode"
       case ${s#line-} in

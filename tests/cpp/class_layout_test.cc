@@ -1,5 +1,8 @@
-// Host check of the score-only layout (gmm_prepare.cc buildClassLayout) against the arithmetic the SCORE_ONLY
-// kernel applies to it (gmm_kernels_i8.hip scoreI8Seg<..., SCORE_ONLY>), without a GPU:
+// Host check of the score-only layouts against the arithmetic their kernels apply to them, without a GPU:
+// the class layout (gmm_prepare.cc buildClassLayout, preselection-batch-int: gmm_kernels_i8.hip
+// scoreI8Seg<..., SCORE_ONLY>) and the slot layout (buildSlotLayout, the other calls without best densities:
+// scoreI8Cls -- every tile gives rows 4g + s and 4g + s + 2 the parity of bit 2g + s of the mixture word, the
+// kernel's minimum is min over (g, s) of 2 min(dot + h) + p).  For the class layout:
 //   * every entry of every mixture sits in exactly one row; padding rows carry the pad constant and zero operands;
 //   * a class tile's rows in lane group g have the parity of bit g of the mixture word, a mixed tile's row
 //     R = 16 i + 4g + r (i-th mixed tile) has parity (R >= er);
@@ -35,7 +38,7 @@ struct Rng {
     }
 };
 
-int check(uint32_t nMix, const std::vector<uint32_t>& counts, uint32_t D, Flavor flavor, uint64_t seed) {
+int check(uint32_t nMix, const std::vector<uint32_t>& counts, uint32_t D, Flavor flavor, uint64_t seed, int kind) {
     Rng                   rng{seed};
     std::vector<uint32_t> off{0};
     for (uint32_t c : counts)
@@ -67,13 +70,13 @@ int check(uint32_t nMix, const std::vector<uint32_t>& counts, uint32_t D, Flavor
     ms.mixture_densities   = dens.data();
     ms.mixture_log_weights = logw.data();
     PreparedQuantized p;
-    const std::string err = prepareQuantized(ms, flavor, ShardRange{0, 0}, p, true);
+    const std::string err = prepareQuantized(ms, flavor, ShardRange{0, 0}, p, kind);
     if (!err.empty()) {
         std::printf("prepareQuantized: %s\n", err.c_str());
         return 1;
     }
-    if (!p.scoreOnly) {
-        std::printf("D=%u: the class layout was not used\n", D);
+    if (p.scoreOnly != kind) {
+        std::printf("D=%u: the score-only layout %d was not used (%d)\n", D, kind, p.scoreOnly);
         return 1;
     }
     const Tiling& t  = p.tiling;
@@ -92,8 +95,30 @@ int check(uint32_t nMix, const std::vector<uint32_t>& counts, uint32_t D, Flavor
     }
     // coverage and parity rules
     std::vector<int> seen(N, 0);
+    const bool       slots = kind == kScoreOnlySlots;
     for (uint32_t m = 0; m < nMix; ++m) {
-        const uint32_t w = p.mixOddMask[m], nc = w >> 16, er = (w >> 4) & 0xfffu;
+        const uint32_t w = p.mixOddMask[m], nc = slots ? t.mixTileOffset[m + 1] - t.mixTileOffset[m] : w >> 16,
+                       er = slots ? 0u : (w >> 4) & 0xfffu;
+        if (slots && (w >> 8) != 0) {
+            std::printf("mixture %u: slot word %08x\n", m, w);
+            return 1;
+        }
+        if (slots) {  // the tile count is the smallest that holds both parities (2 rows per class and tile)
+            uint32_t nE = 0, nO = 0;
+            for (uint32_t x = off[m]; x < off[m + 1]; ++x)
+                (Q[x] & 1 ? nO : nE) += 1;
+            const auto fits = [&](uint32_t T) {
+                for (uint32_t e = 0; e <= 8; ++e)
+                    if (2 * e * T >= nE && 2 * (8 - e) * T >= nO)
+                        return true;
+                return false;
+            };
+            const uint32_t T = nc, ev = static_cast<uint32_t>(__builtin_popcount(~w & 0xffu));
+            if (!fits(T) || (T > 0 && fits(T - 1)) || 2 * ev * T < nE || 2 * (8 - ev) * T < nO) {
+                std::printf("mixture %u: %u tiles for %u even / %u odd rows (%u even classes)\n", m, T, nE, nO, ev);
+                return 1;
+            }
+        }
         const uint32_t t0 = t.mixTileOffset[m], t1 = t.mixTileOffset[m + 1];
         if (t0 + nc > t1) {
             std::printf("mixture %u: %u class tiles of %u\n", m, nc, t1 - t0);
@@ -115,7 +140,9 @@ int check(uint32_t nMix, const std::vector<uint32_t>& counts, uint32_t D, Flavor
                     return 1;
                 }
                 const uint32_t par = static_cast<uint32_t>(Q[x] & 1);
-                const uint32_t want = tile < t0 + nc ? (w >> (r / 4)) & 1u : ((tile - t0 - nc) * 16 + r >= er ? 1u : 0u);
+                const uint32_t want = slots ? (w >> (2 * (r / 4) + (r & 1))) & 1u
+                                            : tile < t0 + nc ? (w >> (r / 4)) & 1u
+                                                             : ((tile - t0 - nc) * 16 + r >= er ? 1u : 0u);
                 if (par != want || h != static_cast<int32_t>(Q[x] >> 1)) {
                     std::printf("mixture %u tile %u row %u: parity %u, expected %u (h %d)\n", m, tile, r, par, want, h);
                     return 1;
@@ -146,6 +173,27 @@ int check(uint32_t nMix, const std::vector<uint32_t>& counts, uint32_t D, Flavor
             const uint32_t w = p.mixOddMask[m], nc = w >> 16, er = (w >> 4) & 0xfffu;
             const uint32_t t0 = t.mixTileOffset[m], t1 = t.mixTileOffset[m + 1];
             int64_t        kern = INT64_MAX;
+            if (slots) {  // scoreI8Cls: per register (g, s) the min of dot + h over rows 4g + s, 4g + s + 2 of every tile
+                for (uint32_t c = 0; c < 8; ++c) {
+                    int64_t vmin = 0x3fffffff;
+                    for (uint32_t tile = t0; tile < t1; ++tile)
+                        for (uint32_t r = 4 * (c / 2) + c % 2; r < 4 * (c / 2) + 4; r += 2) {
+                            int64_t dot = 0;
+                            for (uint32_t k = 0; k < D; ++k) {
+                                const uint32_t lane = (k / 16) * 16 + r, j = k % 16;
+                                dot += static_cast<int64_t>(p.tileA[(static_cast<size_t>(tile) * kLanes + lane) * 16 + j]) * b[k];
+                            }
+                            vmin = std::min(vmin, dot + p.tileP[static_cast<size_t>(tile) * kTileRows + r]);
+                        }
+                    kern = std::min(kern, 2 * vmin + ((w >> c) & 1u));
+                }
+                if (off[m] != off[m + 1] && kern != direct) {
+                    std::printf("slots D=%u mixture %u (%u entries) frame %d: kernel %lld, direct %lld\n", D, m,
+                                off[m + 1] - off[m], f, static_cast<long long>(kern), static_cast<long long>(direct));
+                    return 1;
+                }
+                continue;
+            }
             for (uint32_t g = 0; g < 4; ++g) {  // one lane group: its class minimum in the v domain
                 int64_t vmin = 0x3fffffff;
                 for (uint32_t tile = t0; tile < t0 + nc; ++tile)
@@ -192,11 +240,13 @@ int main() {
             tiny.push_back(static_cast<uint32_t>(rng.next() % 10));
         for (int m = 0; m < 60; ++m)
             big.push_back(160);
-        for (Flavor fl : {Flavor::Simd, Flavor::BatchInt})
-            for (const auto* c : {&ragged, &tiny, &big})
-                if (check(static_cast<uint32_t>(c->size()), *c, D, fl, D * 7 + c->size()) != 0)
-                    return 1;
+        for (int kind : {kScoreOnlyClass, kScoreOnlySlots})
+            for (Flavor fl : {Flavor::Simd, Flavor::BatchInt})
+                for (const auto* c : {&ragged, &tiny, &big})
+                    if (check(static_cast<uint32_t>(c->size()), *c, D, fl, D * 7 + c->size(), kind) != 0)
+                        return 1;
     }
+
     std::printf("ok\n");
     return 0;
 }
