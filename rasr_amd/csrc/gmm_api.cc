@@ -153,7 +153,7 @@ struct gmm_scorer {
     DensityClustering       clustering;
     void*                   dClusterMeans = nullptr;
     uint32_t*               dSelT         = nullptr;  // [nFramesPad/64][clusters][16]
-    uint16_t*               dSelC         = nullptr;  // quantized: [nFramesPad/128][clusters][16] wave-table entries
+    uint8_t*                dSelC         = nullptr;  // quantized: [nFramesPad/128][clusters][16] wave-table entries
     void*                   dTileClu      = nullptr;  // [tiles + pad][16]: u16 cluster * 64 (float), u32 cluster * 16 (int)
     uint32_t                lastFrames    = 0;
     // quantized scalars
@@ -611,7 +611,8 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
     };
     int rc;
     if (s->quantized) {
-        const uint32_t        per = 16u * kI8PreselEntryBytes;
+        // the slot kernel's LDS entries are u16 (the LUT byte offset), the key-layout kernel's u8
+        const uint32_t        per = 16u * (s->scoreOnly == kScoreOnlySlots ? 2u : kI8PreselEntryBytes);
         std::vector<uint32_t> clu(static_cast<size_t>(T + kTilePad) * kTileRows, dc.nClusters * per);
         for (uint32_t t = 0; t < T; ++t)
             for (uint32_t r = 0; r < kTileRows; ++r)
@@ -641,7 +642,7 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
     GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dSelT), selBytes));
     GMM_HIP_CHECK(hipMemset(s->dSelT, 0xff, selBytes));
     if (s->quantized && kI8PreselNF == 8) {
-        const size_t cBytes = static_cast<size_t>(s->nFramesPad / 128) * dc.nClusters * 16 * sizeof(uint16_t);
+        const size_t cBytes = static_cast<size_t>(s->nFramesPad / 128) * dc.nClusters * 16;
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dSelC), cBytes));
         GMM_HIP_CHECK(hipMemset(s->dSelC, 0, cBytes));
     }
@@ -1272,12 +1273,11 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
         PreparedQuantized p;
         // batch types have no best densities: the score-only class layout where it applies
         // (preselection-batch-int included: the kernel masks the class layout's candidates)
-        // (preselection-batch-int masks the class layout's candidates; the others run the slot layout)
+        // (preselection-batch-int included: the kernel masks the slot layout's candidates)
         const bool        scoreOnlyLayout =
                 classLayout || (flavor == Flavor::BatchInt && !(cfg.flags & GMM_FLAG_FULL_KEYS));
         std::string       err = prepareQuantized(*ms, flavor, shard, p,
-                                                 !scoreOnlyLayout ? kScoreOnlyNone
-                                                                  : (presel ? kScoreOnlyClass : kScoreOnlySlots));
+                                                 scoreOnlyLayout ? kScoreOnlySlots : kScoreOnlyNone);
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
         s->scoreOnly = p.scoreOnly;

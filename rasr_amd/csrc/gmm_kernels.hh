@@ -64,7 +64,7 @@ struct I8Args {
     int             finDivide;    // 1: scales outside the range of the multiply-and-correct finalize, divide
     // preselection-batch-int (gmm_kernels_presel.hip): per-(frame, cluster) mask, per-row cluster offsets
     const uint32_t* selT;         // [nFramesPad/64][nClusters][16] u32, byte (frame%64)/16 = 0xff: deselected
-    const uint16_t* selC;         // [nFramesPad/128][nClusters][16] u16: the wave tables (launchCompactSelection)
+    const uint8_t*  selC;         // [nFramesPad/128][nClusters][16] u8: the wave tables (launchCompactSelection)
     const void*     tileClu;      // u32 [T+pad][16]: cluster * 16 * kI8PreselEntryBytes (byte offset into a wave's table)
     uint32_t        nClusters;
     int             presel;
@@ -196,7 +196,7 @@ constexpr uint32_t kI8DummyTileBytes(int ks, bool presel) { return static_cast<u
 // preselection-batch-int: frames per wave / 16 (8: two 64-frame mask words per wave; 4 kept for A/B)
 constexpr uint32_t kI8PreselNF           = GMM_I8_PRESEL_NF;
 // bytes of a mask table entry (gmm_kernels_i8.hip): a row's cluster offset is cluster * 16 * this
-constexpr uint32_t kI8PreselEntryBytes   = kI8PreselNF == 8 ? 2 : 1;
+constexpr uint32_t kI8PreselEntryBytes   = 1;
 constexpr uint32_t kI8PreselFramesPerBlock = kWavesPerBlock * kI8PreselNF * 16;
 
 // density-sharded exchange (gmm_kernels_shard.hip): (score, density) <-> order-preserving int64 keys
@@ -222,8 +222,8 @@ hipError_t launchSelectClusters(bool quantized, const float* frames, uint32_t nF
                                 uint32_t nFramesRead, uint32_t D, uint32_t Dp, const float* variance,
                                 const void* clusterMeans, uint32_t nClusters, uint32_t nSelected, uint32_t* selT,
                                 hipStream_t stream);
-// the quantized scorer's mask table: [nFramesRead / 128][nClusters][16] u16 entries from the byte mask
-hipError_t launchCompactSelection(const uint32_t* selT, uint32_t nFramesRead, uint32_t nClusters, uint16_t* selC,
+// the quantized scorer's mask table: [nFramesRead / 128][nClusters][16] u8 entries from the byte mask
+hipError_t launchCompactSelection(const uint32_t* selT, uint32_t nFramesRead, uint32_t nClusters, uint8_t* selC,
                                   hipStream_t stream);
 hipError_t launchScoreF32(const F32Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void prepareFramesI8(const float* __restrict__
 // ---------------------------------------------------------------------------
 // Finalize and store the per-mixture minima: lane `lane` holds, in res[i], the packed (score, density) minimum
 // of frame frame0 + 64 i + lane (both quantized kernels leave their reduce-scatter in this order).
-template <int NPL, bool MAYBE_NONE>
+template <int NPL, bool MAYBE_NONE, int NONE_FROM = INT_MAX>
 __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restrict__ scores,
                                                 uint32_t* __restrict__ bestOut, const int (&res)[NPL], uint32_t m,
                                                 uint32_t frame0, int lane, int ib, const int (&ssOut)[NPL]) {
@@ -106,7 +106,7 @@ __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restri
         const uint32_t f = frame0 + 64 * i + lane;
         const int packed = res[i];
         // mixture without densities: minScore stays Core::Type<int>::max
-        const bool     none = MAYBE_NONE && packed == INT_MAX;
+        const bool     none = MAYBE_NONE && packed >= NONE_FROM;
         const int      q    = none ? INT_MAX : (packed >> ib) + ssOut[i];
         const uint32_t dns  = none ? 0xffffffffu : static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
         // Both reference finalizes divide by b = 2 s^2: SimdFeatureScorer.cc:142 (f32)(0.5 * q / (f64)s2) and
@@ -138,7 +138,7 @@ __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restri
 // never reaches INT_MAX otherwise (the host bounds every real row's packed value below 2^31 - 2^(ib+1),
 // gmm_prepare.cc), so the scorer's per-mixture emit skips those selects (v_cndmask issues at a
 // quarter of the rate of the other VALU ops).
-template <int NF, bool MAYBE_NONE = true, int S = 4>
+template <int NF, bool MAYBE_NONE = true, int S = 4, int NONE_FROM = INT_MAX>
 __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict__ scores, uint32_t* __restrict__ bestOut,
                                               const int (&best)[NF][S], uint32_t m, uint32_t frame0, int lane, int g,
                                               int ib, const int (&ssOut)[NF / 4]) {
@@ -169,7 +169,7 @@ __device__ __forceinline__ void emitMixtureI8(const I8Args& a, float* __restrict
     for (int i = 0; i < NPL; ++i)
         res[i] = swapMin16(w[2 * i], w[2 * i + 1]);
 
-    finalizeStoreI8<NPL, MAYBE_NONE>(a, scores, bestOut, res, m, frame0, lane, ib, ssOut);
+    finalizeStoreI8<NPL, MAYBE_NONE, NONE_FROM>(a, scores, bestOut, res, m, frame0, lane, ib, ssOut);
 }
 
 template <int NF, int KS, bool MULTI>
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
     static_assert(!PRESEL || NF == 4 || NF == 8, "preselection masks: one or two 64-frame words per wave");
     // PRESEL mask table entries: NF 4 a byte (4 deselection bits x 4: the byte offset of a u32 in maskLut), NF 8 a
     // u16 (8 bits x 8: the byte offset of a u64 in maskLut)
-    constexpr uint32_t kEntryBytes = NF == 8 ? 2u : 1u;
+    constexpr uint32_t kEntryBytes = 1u;
     typedef typename std::conditional<NF == 8, uint64_t, uint32_t>::type LutW;  // a maskLut entry
     typedef uint2 MaskW;  // a row's mask bytes as registers: x blocks 0-3, y blocks 4-7 (NF 8)
     static_assert(!SCORE_ONLY || KS == 1, "score-only layout: one K step");
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
         // the wave's 128 frames' table, built once per call (launchCompactSelection), by LDS-DMA ahead of the ring
         // (the oldest vector-memory operations: the first segment's counted wait covers them)
         const int8_t*  src   = reinterpret_cast<const int8_t*>(a.selC + static_cast<size_t>(frame0 / 128u) * words);
-        const uint32_t bytes = words * 2u;
+        const uint32_t bytes = words;
         for (uint32_t off = 0; off < bytes; off += 1024u)
             if (off + static_cast<uint32_t>(lane) * 16u < bytes)
                 __builtin_amdgcn_global_load_lds(src + off + lane * 16, lds + tabOff + off, 16, 0, 0);
@@ -517,11 +517,10 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
                 reinterpret_cast<uint32_t*>(lds + tabOff)[i] = packed;
             }
         }
-        // the never-selected cluster: every frame deselected, in all 16 columns
+        // the never-selected cluster: every frame deselected, in all 16 columns (NF 8: LUT index 255; NF 4: byte
+        // offset 4 * 15)
         if (lane < 4)
-            reinterpret_cast<uint32_t*>(lds + tabOff + words * kEntryBytes)[lane] = NF == 8 ? 0x07f807f8u : 0x3c3c3c3cu;
-        if (NF == 8 && lane >= 4 && lane < 8)
-            reinterpret_cast<uint32_t*>(lds + tabOff + words * kEntryBytes)[lane] = 0x07f807f8u;
+            reinterpret_cast<uint32_t*>(lds + tabOff + words * kEntryBytes)[lane] = NF == 8 ? 0xffffffffu : 0x3c3c3c3cu;
         laneSel = tabOff + (static_cast<uint32_t>(lane) & 15u) * kEntryBytes;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LUT and entries before the first segment's barrier
     }
@@ -539,10 +538,9 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
             const int8_t* lu = reinterpret_cast<const int8_t*>(maskLut);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t e = NF == 8 ? *reinterpret_cast<const uint16_t*>(tb + c4[j])
-                                           : *reinterpret_cast<const uint8_t*>(tb + c4[j]);
-                if constexpr (NF == 8)
-                    T[j] = *reinterpret_cast<const uint2*>(lu + e);
+                const uint32_t e = *reinterpret_cast<const uint8_t*>(tb + c4[j]);
+                if constexpr (NF == 8)  // e: the LUT index (the 8 deselection bits)
+                    T[j] = *reinterpret_cast<const uint2*>(lu + e * 8u);
                 else
                     T[j] = uint2{*reinterpret_cast<const uint32_t*>(lu + e), 0u};
             }
@@ -884,25 +882,51 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
 #ifndef GMM_I8_CLS_LAG
 #define GMM_I8_CLS_LAG 3  // column blocks whose epilogue runs one step late
 #endif
+#ifndef GMM_I8_PRESEL_CPF
+#define GMM_I8_PRESEL_CPF 1  // preselection: the rows' cluster offsets read one tile ahead with the operands
+#endif
+#ifndef GMM_I8_PRESEL_WAVES
+#define GMM_I8_PRESEL_WAVES 3  // preselection: waves per SIMD the register allocation must allow
+#endif
 #ifndef GMM_I8_CLS_DIAG
 #define GMM_I8_CLS_DIAG 0  // timing diagnostics only (wrong results): 1 = no per-mixture emit (the last one aside)
 #endif
-template <int NF, int SEG, int W>
-__global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, const uint32_t* __restrict__ mixTileOff,
-                                                                    float* __restrict__ scores,
-                                                                    const uint32_t* __restrict__ mixWord) {
+// PRESEL (preselection-batch-int, NF 8): the row constants are biased by 2^31 (the accumulator u = v + 2^31 is
+// compared unsigned) and every candidate is OR-ed with the sign-extended mask byte of its (frame, row cluster), so a
+// density whose cluster the frame did not select becomes all ones and never wins; padding rows sit in an extra
+// never-selected cluster.  Per tile the lane reads its 4 rows' table entries (the wave's [cluster][t] table of
+// launchCompactSelection, copied to LDS by LDS-DMA at the start) and their LUT expansions to 8 mask bytes, one per
+// column block; the tile's epilogues follow its MFMAs in the same step (no pending tail).  A frame that selected
+// none of a mixture's densities keeps all ones: Core::Type<int>::max, as the reference.
+template <int NF, int SEG, int W, bool PRESEL = false>
+__global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : 4) : 1) void scoreI8Cls(I8Args a, const uint32_t* __restrict__ mixTileOff,
+                                                                                   float* __restrict__ scores,
+                                                                                   const uint32_t* __restrict__ mixWord) {
     static_assert(NF == 4 || NF == 8, "NF");
-    constexpr int      LAG       = GMM_I8_CLS_LAG;
+    static_assert(!PRESEL || (NF == 8 && W == 4), "preselection: 128-frame waves (two 64-frame mask words)");
+    constexpr int      LAG       = PRESEL ? 0 : GMM_I8_CLS_LAG;
     constexpr int      NPL       = NF / 4;
     constexpr uint32_t kSegA     = SEG * 1024u;
-    constexpr uint32_t kSegBytes = kSegA + SEG * 64u;
+    constexpr uint32_t kSegP     = kSegA + SEG * 64u;
+    constexpr uint32_t kSegBytes = kSegP + (PRESEL ? SEG * 64u : 0u);  // + the rows' cluster offsets (u32)
     constexpr int      kPieces   = SEG / W;          // 1 KiB operand pieces per wave per segment
     constexpr uint32_t kRowLanes = 4u * SEG / W;     // lanes loading 16 B of row constants per wave
-    constexpr int      kIssued   = kPieces + 1;
-    constexpr int      kNeutral  = 0x3fffffff;       // above every row (padding rows: 0x30000000)
-    static_assert(SEG % W == 0 && kRowLanes <= 64 && LAG >= 1 && LAG < NF, "segment / lag");
-    // + 64: the look-ahead read past the last tile of buffer 1 stays inside the array
-    __shared__ __attribute__((aligned(16))) int8_t lds[2 * kSegBytes + 64];
+    constexpr int      kIssued   = kPieces + 1 + (PRESEL ? 1 : 0);
+    constexpr int      kNeutral  = PRESEL ? -1 : 0x3fffffff;  // above every row (padding rows: 0x30000000)
+    static_assert(SEG % W == 0 && kRowLanes <= 64 && (PRESEL || (LAG >= 1 && LAG < NF)), "segment / lag");
+    // + 64: the look-ahead read past the last tile of buffer 1 stays inside the array.  PRESEL: ring and the waves'
+    // mask tables in the dynamic array, the 256-entry LUT static (its address folds into the reads)
+    int8_t* lds;
+    int8_t* lut = nullptr;
+    if constexpr (PRESEL) {
+        __shared__ uint64_t lutStatic[256];
+        lds = i8DynLds;
+        lut = reinterpret_cast<int8_t*>(lutStatic);
+    }
+    else {
+        __shared__ __attribute__((aligned(16))) int8_t ldsStatic[2 * kSegBytes + 64];
+        lds = ldsStatic;
+    }
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -929,11 +953,64 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
         if (lane < kRowLanes)
             __builtin_amdgcn_global_load_lds(gP + static_cast<size_t>(t0) * 64 + wave * (kRowLanes * 16) + lane * 16,
                                              base + kSegA + wave * (kRowLanes * 16), 16, 0, 0);
+        if constexpr (PRESEL) {
+            if (lane < kRowLanes)
+                __builtin_amdgcn_global_load_lds(static_cast<const int8_t*>(a.tileClu) + static_cast<size_t>(t0) * 64 +
+                                                         wave * (kRowLanes * 16) + lane * 16,
+                                                 base + kSegP + wave * (kRowLanes * 16), 16, 0, 0);
+        }
     };
+    // PRESEL: this wave's mask table [cluster][16] (+ the never-selected cluster) after the ring, by LDS-DMA ahead
+    // of the ring (the oldest vector-memory operations: the first segment's counted wait covers them)
+    // In LDS a table entry is the u16 byte offset 8 e of the LUT entry (no scaling per read); in global memory the
+    // per-call table holds e itself (one byte: what every chunk's workgroups re-read stays in L2), so each wave
+    // loads its 4 KiB (256 clusters) once into registers and expands it
+    const uint32_t words  = PRESEL ? a.nClusters * 16u : 0u;  // entries (cluster, t)
+    const uint32_t tabOff = 2 * kSegBytes + 64u + static_cast<uint32_t>(wave) * (words + 16u) * 2u;
+    constexpr int  kTabV  = PRESEL ? 4 : 1;  // 16-byte pieces of the table per lane (<= 256 clusters)
+    i32x4          tabV[kTabV];
+    if constexpr (PRESEL) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(a.selC + static_cast<size_t>(frame0 / 128u) * words);
+#pragma unroll
+        for (int i = 0; i < kTabV; ++i)
+            if ((i * 64u + static_cast<uint32_t>(lane)) * 16u < words)
+                tabV[i] = src[i * 64 + lane];
+    }
     if (nSeg > 0)
         issueSeg(0);
     if (nSeg > 1)
         issueSeg(1);
+    uint32_t laneSel = 0;  // PRESEL: byte offset of (wave table, column t = lane & 15)
+    if constexpr (PRESEL) {
+        for (uint32_t n = threadIdx.x; n < 256u; n += 64u * W) {  // entry n (8 deselection bits) -> 8 mask bytes
+            uint64_t v = 0;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb)
+                v |= ((n >> cb) & 1u) ? uint64_t(0xff) << (8 * cb) : uint64_t(0);
+            reinterpret_cast<uint64_t*>(lut)[n] = v;
+        }
+        // expand: bytes b0 b1 b2 b3 of a word -> u16 pairs (8 b0, 8 b1), (8 b2, 8 b3): LUT byte offsets
+#pragma unroll
+        for (int i = 0; i < kTabV; ++i) {
+            const uint32_t q = i * 64u + static_cast<uint32_t>(lane);
+            if (q * 16u >= words)
+                continue;
+            uint32_t o[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t w = static_cast<uint32_t>(tabV[i][j]);
+                o[2 * j]         = ((w & 0xffu) | ((w & 0xff00u) << 8)) << 3;
+                o[2 * j + 1]     = (((w >> 16) & 0xffu) | ((w >> 8) & 0xff0000u)) << 3;
+            }
+            uint4* dst = reinterpret_cast<uint4*>(lds + tabOff + q * 32u);
+            dst[0]     = uint4{o[0], o[1], o[2], o[3]};
+            dst[1]     = uint4{o[4], o[5], o[6], o[7]};
+        }
+        if (lane < 8)  // the never-selected cluster: every frame deselected (LUT entry 255: byte offset 2040)
+            reinterpret_cast<uint32_t*>(lds + tabOff + words * 2u)[lane] = 0x07f807f8u;
+        laneSel = tabOff + (static_cast<uint32_t>(lane) & 15u) * 2u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LUT and entries before the first segment's barrier
+    }
 
     i32x4 B[NF];
 #pragma unroll
@@ -943,6 +1020,8 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
 #pragma unroll
     for (int i = 0; i < NPL; ++i)
         ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
+    if constexpr (PRESEL)  // every load before the ring (frame operands, table, the first segments) complete: the
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // waitcnt pass then leaves the loop without vmcnt waits (vmcnt(0))
 
     // mixture m ends at tile tEnd; its word wCur and the next mixture's end tNext are loaded one mixture ahead
     // (scalar loads whose latency the mixture's steps cover)
@@ -963,11 +1042,51 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
     const auto epiSet = [&](int cb) {  // a mixture's first tile: the minima start from its candidates
         best[cb] = i32x2{min(acc[cb][0], acc[cb][2]), min(acc[cb][1], acc[cb][3])};
     };
+    // PRESEL: candidate (block cb, row r) OR the sign-extended mask byte cb of the row (one v_or_b32_sdwa), the
+    // biased keys compared unsigned
+    typedef uint2 MaskW;  // a row's 8 mask bytes: x blocks 0-3, y blocks 4-7
+    const auto cand = [&](int cb, int r, const MaskW (&T)[4]) -> uint32_t {
+        const uint32_t h = cb >= 4 ? T[r].y : T[r].x;
+        return static_cast<uint32_t>(acc[cb][r]) |
+               static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(h >> (8 * (cb & 3)))));
+    };
+    const auto epiMask = [&](int cb, const MaskW (&T)[4], bool set) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            uint32_t b = min(cand(cb, s2, T), cand(cb, s2 + 2, T));
+            if (!set)
+                b = min(static_cast<uint32_t>(best[cb][s2]), b);
+            asm volatile("" : "+v"(b));
+            best[cb][s2] = static_cast<int>(b);
+        }
+    };
     // per-mixture emit: 2 min(v) + p per register (p = bit 2g + s of the word), the lane's two registers merged,
     // the reduce-scatter over the lane groups, finalize and store
     const auto emit = [&](uint32_t mm) {
         const uint32_t w = wCur;
         int            v[NF][1];
+        if constexpr (PRESEL) {
+            // biased u = v + 2^31, clamped at 2^31 + 2^29 (all ones: nothing selected); 2 u + p = 2 v + p modulo 2^32
+            // (the bias shifts out), and a clamped register gives 2^30 + p, reported as none
+            constexpr uint32_t kClamp = 0x80000000u + (1u << 29);
+            if (((w ^ (w >> 1)) & 0x55u) == 0u) {  // both registers of every lane group share the parity (uniform)
+                const uint32_t p = (w >> (2 * g)) & 1u;
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb) {
+                    const uint32_t u = min(min(static_cast<uint32_t>(best[cb][0]), static_cast<uint32_t>(best[cb][1])), kClamp);
+                    v[cb][0]         = static_cast<int>((u << 1) + p);
+                }
+            }
+            else {
+                const uint32_t p0 = (w >> (2 * g)) & 1u, p1 = (w >> (2 * g + 1)) & 1u;
+#pragma unroll
+                for (int cb = 0; cb < NF; ++cb)
+                    v[cb][0] = min(static_cast<int>((min(static_cast<uint32_t>(best[cb][0]), kClamp) << 1) + p0),
+                                   static_cast<int>((min(static_cast<uint32_t>(best[cb][1]), kClamp) << 1) + p1));
+            }
+            emitMixtureI8<NF, true, 1, (1 << 30)>(a, scores, nullptr, v, mm, frame0, lane, g, 0, ssOut);
+            return;
+        }
         if (((w ^ (w >> 1)) & 0x55u) == 0u) {  // both registers of every lane group share the parity (uniform)
             const int p = static_cast<int>((w >> (2 * g)) & 1u);
 #pragma unroll
@@ -1011,8 +1130,41 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
     // the step of one tile: MFMA of block cb beside the epilogue of block cb - LAG (of the previous step for cb <
     // LAG), fenced so the scheduler keeps that pairing.  FIRST: the first tile of a mixture (after boundary()): no
     // pending tail; its candidates set the minima of its first NF - LAG blocks (no reset of those)
-    const auto step = [&](const i32x4& A, const i32x4& P, uint32_t t, auto firstC) {
+    const auto step = [&](const i32x4& A, const i32x4& P, const i32x4& Cpf, const int8_t* cptr, uint32_t t,
+                          auto firstC, auto prefetch) {
         constexpr bool kFirst = decltype(firstC)::value;
+        (void)cptr;
+        if constexpr (!PRESEL)
+            prefetch();
+        if constexpr (PRESEL) {
+            // the tile's mask rows: the lane's table entries (LUT indices), then their 8 mask bytes; the rows'
+            // cluster offsets prefetched with the operands (GMM_I8_PRESEL_CPF) or read here
+            i32x4 C = Cpf;
+            if constexpr (!GMM_I8_PRESEL_CPF)
+                C = *reinterpret_cast<const i32x4*>(cptr);
+            // The LUT reads are inline asm: a compiler-visible 64-bit LDS read at a loaded address makes the
+            // waitcnt pass drain the LDS-DMA queue (s_waitcnt vmcnt(0)) at every step, since it cannot tell the
+            // read from the ring the DMA fills; their lgkmcnt wait is explicit, before the epilogues
+            // (the 64-bit LUT read makes the waitcnt pass wait for the LDS-DMA queue, s_waitcnt vmcnt(0): by then
+            // the next segment, issued a segment ahead, has landed; two 32-bit reads from split tables avoid the
+            // wait but measured 11 % slower, profiles/r05/s9)
+            prefetch();
+            MaskW T[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t e = *reinterpret_cast<const uint16_t*>(lds + laneSel + static_cast<uint32_t>(C[r]));
+                T[r]             = *reinterpret_cast<const MaskW*>(lut + e);
+            }
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                acc[cb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B[cb], P, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                epiMask(cb, T, kFirst);
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+        }
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb) {
             __builtin_amdgcn_sched_barrier(0);
@@ -1033,13 +1185,17 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
     // mixture m ends at tile t and another with tiles follows: the pending tail completes m, which is emitted; the
     // tail's minima restart above every row (the next mixture's first step sets the others)
     const auto boundary = [&](uint32_t t) {
+        if constexpr (!PRESEL) {
 #pragma unroll
-        for (int cb = NF - LAG; cb < NF; ++cb)
-            epiMin(cb);
+            for (int cb = NF - LAG; cb < NF; ++cb)
+                epiMin(cb);
+        }
         finish(t);
+        if constexpr (!PRESEL) {
 #pragma unroll
-        for (int cb = NF - LAG; cb < NF; ++cb)
-            asm volatile("v_mov_b64 %0, %1" : "=v"(best[cb]) : "s"(kNeutral2));
+            for (int cb = NF - LAG; cb < NF; ++cb)
+                asm volatile("v_mov_b64 %0, %1" : "=v"(best[cb]) : "s"(kNeutral2));
+        }
     };
     const std::true_type  kFirstTile{};
     const std::false_type kInner{};
@@ -1070,19 +1226,23 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
         // this lane's operand addresses of the current tile t; tile t + i is i KiB (A) and i * 64 B (P) further
         const int8_t* pa = base + lane * 16;
         const int8_t* pp = base + kSegA + g * 16;
-        const auto    rd = [&](int i, i32x4& A, i32x4& P) {  // (past the segment: read, never used)
+        // PRESEL: the lane group's 4 row cluster offsets, as one aligned 16-byte read
+        const auto rd = [&](int i, i32x4& A, i32x4& P, i32x4& C) {  // (past the segment: read, never used)
             A = *reinterpret_cast<const i32x4*>(pa + i * 1024);
             P = *reinterpret_cast<const i32x4*>(pp + i * 64);
+            if constexpr (PRESEL && GMM_I8_PRESEL_CPF)
+                C = *reinterpret_cast<const i32x4*>(pp + (kSegP - kSegA) + i * 64);
         };
-        i32x4    A0, P0, A1, P1;  // tile t, and the next one in flight
+        const auto cp = [&](int i) { return pp + (kSegP - kSegA) + i * 64; };  // the tile's cluster offsets
+        i32x4    A0, P0, C0, A1, P1, C1;  // tile t, and the next one in flight
         uint32_t t = segT0;
-        rd(0, A0, P0);
+        rd(0, A0, P0, C0);
         while (t < segEnd) {
             if (fresh) {  // the first tile of a mixture
-                rd(1, A1, P1);
-                step(A0, P0, t, kFirstTile);
+                step(A0, P0, C0, cp(0), t, kFirstTile, [&] { rd(1, A1, P1, C1); });
                 A0 = A1;
                 P0 = P1;
+                C0 = C1;
                 pa += 1024;
                 pp += 64;
                 ++t;
@@ -1091,18 +1251,16 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
             const uint32_t mEnd = min(segEnd, tEnd);
             // two tiles per iteration on alternating registers (no copies of the operands in flight)
             for (; t + 2 <= mEnd; t += 2) {
-                rd(1, A1, P1);
-                step(A0, P0, t, kInner);
-                rd(2, A0, P0);
-                step(A1, P1, t + 1, kInner);
+                step(A0, P0, C0, cp(0), t, kInner, [&] { rd(1, A1, P1, C1); });
+                step(A1, P1, C1, cp(1), t + 1, kInner, [&] { rd(2, A0, P0, C0); });
                 pa += 2048;
                 pp += 128;
             }
             if (t < mEnd) {
-                rd(1, A1, P1);
-                step(A0, P0, t, kInner);
+                step(A0, P0, C0, cp(0), t, kInner, [&] { rd(1, A1, P1, C1); });
                 A0 = A1;
                 P0 = P1;
+                C0 = C1;
                 pa += 1024;
                 pp += 64;
                 ++t;
@@ -1121,7 +1279,7 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 4 : 1) void scoreI8Cls(I8Args a, c
     if (m < m1) {
 #pragma unroll
         for (int cb = NF - LAG; cb < NF; ++cb)
-            epiMin(cb);
+            epiMin(cb);  // (PRESEL: LAG 0, none)
         emit(m);
         advance();
         while (m < m1) {
@@ -1148,6 +1306,18 @@ template <int NF, int KS, bool MULTI, int W = 4>
 static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
 #if GMM_I8_LDS
     if constexpr (!MULTI) {
+        if (a.presel && a.scoreOnly == 2) {  // preselection-batch-int on the slot layout (3 waves per SIMD: registers)
+            if constexpr (KS == 1 && kI8PreselNF == 8) {
+                constexpr int      kSeg = 4;
+                constexpr uint32_t kRing = 2 * kSeg * (1024 + 64 + 64) + 64;
+                const uint32_t     lds   = kRing + 4u * (a.nClusters * 16u + 16u) * 2u;
+                constexpr int      kMax  = static_cast<int>(kRing + 4u * (256u * 16u + 16u) * 2u);
+                (void)allowDynamicLds(reinterpret_cast<const void*>(&dev::scoreI8Cls<8, kSeg, 4, true>), kMax);
+                hipLaunchKernelGGL((dev::scoreI8Cls<8, kSeg, 4, true>), dim3(grid), dim3(256), lds, s, a, a.mixTileOff,
+                                   a.scores, a.mixOddMask);
+            }
+            return;
+        }
         if (a.presel) {  // preselection-batch-int: NF 4, 4-tile segments (ring + 4 mask tables < 80 KiB)
             constexpr int      kSeg  = 4;
             constexpr uint32_t kRing = 2 * (kSeg * (KS * 1024 + 64 + 64)) + kI8DummyTileBytes(KS, true);

@@ -180,14 +180,14 @@ __global__ __launch_bounds__(256) void selectClusters(const float* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // the quantized scorer's per-wave mask table (gmm_kernels_i8.hip scoreI8Seg<PRESEL>, 128 frames per wave), built
-// once per call from the byte mask: for every group of 128 frames, cluster c and t = frame % 16 one u16 entry
-// 8 * (bit j: frame 16 j + t of the group did not select c), j = 0..7 -- the byte offset of the u64 in the scorer's
-// LDS look-up table that expands the 8 bits into one 0x00 / 0xff byte per column block.  8 KiB per 128 frames at
-// 256 clusters (a quarter of the byte mask, which every chunk's workgroups would otherwise re-read and compress):
-// the whole table of a 32768-frame call stays in an XCD's L2.
+// once per call from the byte mask: for every group of 128 frames, cluster c and t = frame % 16 one byte, bit j:
+// frame 16 j + t of the group did not select c (j = 0..7) -- the index of the u64 in the scorer's LDS look-up table
+// that expands the 8 bits into one 0x00 / 0xff byte per column block.  4 KiB per 128 frames at 256 clusters (an
+// eighth of the byte mask, which every chunk's workgroups would otherwise re-read and compress): with the frame
+// operands, a 32768-frame call's 3 MiB stay in an XCD's L2 while its workgroups walk their chunks.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void compactSelection(const uint32_t* __restrict__ selT, uint32_t nGroups,
-                                                        uint32_t nClusters, uint16_t* __restrict__ selC) {
+                                                        uint32_t nClusters, uint8_t* __restrict__ selC) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;  // (group, cluster, t)
     if (i >= nGroups * nClusters * 16u)
         return;
@@ -195,12 +195,12 @@ __global__ __launch_bounds__(256) void compactSelection(const uint32_t* __restri
     const uint32_t w0 = selT[(static_cast<size_t>(2 * grp) * nClusters + c) * 16u + t];
     const uint32_t w1 = selT[(static_cast<size_t>(2 * grp + 1) * nClusters + c) * 16u + t];
     const auto     nib = [](uint32_t w) { return ((w & 0x01010101u) * 0x01020408u) >> 24 & 0xfu; };  // bit q = byte q
-    selC[i]            = static_cast<uint16_t>((nib(w0) | nib(w1) << 4) * 8u);
+    selC[i]            = static_cast<uint8_t>(nib(w0) | nib(w1) << 4);
 }
 
 }  // namespace dev
 
-hipError_t launchCompactSelection(const uint32_t* selT, uint32_t nFramesRead, uint32_t nClusters, uint16_t* selC,
+hipError_t launchCompactSelection(const uint32_t* selT, uint32_t nFramesRead, uint32_t nClusters, uint8_t* selC,
                                   hipStream_t stream) {
     if (nFramesRead % 128 || nClusters > 256)
         return hipErrorInvalidValue;

@@ -15,6 +15,8 @@ PASSES=(
   "WRITE_SIZE"
   "TCC_HIT_sum TCC_MISS_sum"
 )
+# PMC_EXTRA: one more pass (e.g. "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS")
+[ -n "$PMC_EXTRA" ] && PASSES+=("$PMC_EXTRA")
 i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))
