@@ -24,7 +24,7 @@ LIB       = $(LIBDIR)/librasr_gmm.so
 OBJS      = $(BUILD)/gmm_kernels_i8.o $(BUILD)/gmm_kernels_f32.o $(BUILD)/gmm_kernels_split.o $(BUILD)/gmm_api.o $(BUILD)/gmm_prepare.o \
             $(BUILD)/GpuFeatureScorer.o $(BUILD)/MixtureSetFile.o $(BUILD)/MixtureSetEstimatorFile.o $(BUILD)/nn_kernels.o $(BUILD)/nn_api.o \
             $(BUILD)/gmm_kernels_presel.o $(BUILD)/gmm_presel.o $(BUILD)/gmm_kernels_shard.o $(BUILD)/gmm_hostio.o \
-            $(BUILD)/gmm_kernels_direct.o $(BUILD)/gmm_kernels_layout.o $(BUILD)/gmm_shard.o
+            $(BUILD)/gmm_kernels_direct.o $(BUILD)/gmm_kernels_layout.o $(BUILD)/gmm_shard.o $(BUILD)/gmm_kernels_pairs.o
 DRIVER    = $(BUILD)/tests/feature_scorer_driver
 
 REFSORT   = $(BUILD)/tests/refsort_test
@@ -52,6 +52,11 @@ $(BUILD)/gmm_kernels_presel.o: $(SRC)/gmm_kernels_presel.hip $(SRC)/gmm_refsort.
 # reference-order float scorers (GMM_FLAG_REFERENCE_ORDER): scalar f32 ops in the reference's order
 # (no SLP packing into v_pk_*_f32, which issue at a third of the scalar VOP2 rate)
 $(BUILD)/gmm_kernels_direct.o: $(SRC)/gmm_kernels_direct.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
+
+# sparse best densities of (frame, mixture) pairs (gmm_best_density_pairs): the reference's scalar order
+$(BUILD)/gmm_kernels_pairs.o: $(SRC)/gmm_kernels_pairs.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
 

@@ -627,14 +627,18 @@ def drop_in(args, kind):
     """The C++ drop-in (Mm::Gpu::GpuBatchFeatureScorer / GpuFeatureScorer) driven through the recognizer protocol at
     RASR buffer sizes, PCIe and host bookkeeping included: tests/cpp/feature_scorer_driver.cc's bench mode (a child
     process), consuming every emission's score per frame as FeatureScorerNode does; best densities not read (the
-    search), plus one run reading them (the aligners).  Reported beside the headline, never `value`."""
+    search), plus runs reading them: for every emission (the dump) and for 1-10 emissions per frame (an aligner).
+    Reported beside the headline, never `value`."""
     drv = os.path.join(ROOT, "build", "tests", "feature_scorer_driver")
     if not os.access(drv, os.X_OK):
         return {"error": f"{drv} not built"}
     recs = []
     # (sizes, frames, read best densities, share of emissions read per frame in permille): the dump consumer at
     # every size, the aligners' read, and a search-like consumer reading 10 % of the emissions
-    runs = [(DROP_IN_SIZES, DROP_IN_FRAMES, 0, 1000), ([4096], [262144], 1, 1000), ([512, 4096], [196608, 262144], 0, 100)]
+    # best 2: an aligner's read, bestDensity(e) of 1-10 emissions per frame beside every score (sparse pairs, then
+    # best densities carried by every later call)
+    runs = [(DROP_IN_SIZES, DROP_IN_FRAMES, 0, 1000), ([4096], [262144], 1, 1000), ([1, 512, 4096], [1500, 196608, 262144], 2, 1000),
+            ([512, 4096], [196608, 262144], 0, 100)]
     for sizes, frames, best, permille in runs:
         cmd = [drv, "bench", kind, ",".join(map(str, sizes)), ",".join(map(str, frames)), str(args.mixtures),
                str(args.densities), str(args.dim), str(best), str(permille)]

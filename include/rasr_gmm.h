@@ -201,6 +201,29 @@ int gmm_host_call_wait(gmm_scorer* scorer, uint64_t call_id);
  * host call of this scorer has replaced them (the caller scores those frames again). */
 int gmm_fetch_best_density(gmm_scorer* scorer, uint64_t call_id, uint32_t* best_density, uint32_t score_stride);
 
+/* Sparse best densities: AssigningContextScorer::bestDensity(e) for a LIST of (ring position, mixture) pairs of host
+ * call `call_id` (made with GMM_HOST_KEEP_BEST or GMM_HOST_LAZY_BEST, its frames still on the device), instead of
+ * the whole table gmm_fetch_best_density computes and copies.  best_density[i] receives the density-in-mixture
+ * index for frame positions[i] (a ring position that call scored) and mixture mixtures[i]; 0xffffffff for a
+ * mixture without a finite candidate.  HOST arrays, synchronous (one small kernel; about the latency of one
+ * launch).  The mixture's densities are scored in the reference's own arithmetic and scanned in its order
+ * (AssigningFeatureScorer.hh:110-121, SimdFeatureScorer.cc:135-176, GaussDiagonalMaximumFeatureScorer.cc:116-142,
+ * 263-286): SIMD-diagonal-maximum bit-exact; the float types as the CPU restatement computes them (a near tie may
+ * name another density than the keyed table scorers, within their float contract).  Errors: GMM_ERR_INVALID_ARGUMENT
+ * once a later host call replaced the frames, for a position the call did not score or a mixture out of range;
+ * GMM_ERR_UNSUPPORTED for batch types, density-sharded handles and float models of dimension > 128 (the caller
+ * uses gmm_fetch_best_density).  Replaces the per-emission bestDensity(e) of the reference's context scorers for
+ * callers that ask a few emissions per frame (aligners, AbstractMixtureSetEstimator.cc:370-384). */
+int gmm_best_density_pairs(gmm_scorer* scorer, uint64_t call_id, const uint32_t* positions, const uint32_t* mixtures,
+                           uint32_t n_pairs, uint32_t* best_density);
+
+/* The same for frames in DEVICE memory (row t at frames + t * frame_stride floats, t < n_frames) and DEVICE pair
+ * arrays (pair_frame[i] < n_frames, pair_mixture[i] < the handle's mixtures; an out-of-range pair yields
+ * 0xffffffff), enqueued on `stream` (a hipStream_t; NULL = default stream), asynchronous. */
+int gmm_best_density_pairs_device(gmm_scorer* scorer, const float* frames, uint32_t n_frames, uint32_t frame_stride,
+                                  const uint32_t* pair_frame, const uint32_t* pair_mixture, uint32_t n_pairs,
+                                  uint32_t* best_density, void* stream);
+
 /* Page-locked host memory for gmm_score_host's outputs (the buffer a batched caller keeps, e.g.
  * BatchFeatureScorerBase::scores_, BatchFeatureScorer.hh:177-186), so that callers need no HIP
  * headers.  gmm_host_free(NULL) is a no-op. */

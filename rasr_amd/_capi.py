@@ -119,6 +119,11 @@ PROTOTYPES = [
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     ("gmm_host_call_wait", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     ("gmm_fetch_best_density", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32]),
+    ("gmm_best_density_pairs", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("gmm_best_density_pairs_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     ("gmm_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     ("gmm_host_free", ctypes.c_int, [ctypes.c_void_p]),
     ("gmm_scorer_quantization", ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p]),

@@ -221,15 +221,34 @@ struct gmm_scorer {
     // density table runs (gmm_score_device with best_density NULL, GMM_HOST_LAZY_BEST host calls): the
     // reference's score(e) without the index-carrying pack, bit-identical scores
     std::unique_ptr<gmm_scorer> scoresOnly;
+    // sparse best densities (gmm_best_density_pairs, gmm_kernels_pairs.hip): entry-major tables of the assigning
+    // types in the reference's arithmetic; pairKind -1 where the model has none (e.g. float D > 128)
+    int       pairKind = -1;
+    uint32_t  pairL = 0, pairNb = 0, pairIsvStride = 0;
+    uint32_t* dPairMixOff = nullptr;
+    uint32_t* dPairCov    = nullptr;
+    uint8_t*  dPairQMean  = nullptr;
+    int32_t*  dPairQConst = nullptr;
+    float*    dPairFMean  = nullptr;
+    float*    dPairFConst = nullptr;
+    float*    dPairLogNorm = nullptr;
+    float*    dPairIsv    = nullptr;
+    // host pair lists: a page-locked staging buffer the kernel reads and writes in place (frame, mixture, best)
+    uint32_t* hPairStage   = nullptr;
+    size_t    pairStageCap = 0;  // pairs
 
     ~gmm_scorer() {
         void* ptrs[] = {dTileA,   dTileP,   dTileCov, dRowDns,     dMixTileOff, dIsv,      dFrameQ,
                         dFrameSS, dFrameX,  dFrameXX, dHostFrames, dHostScores, dHostBest, dFrameH,
                         dFrameExp, dDimScale, dLimbExp, dClusterMeans, dSelT, dSelC, dTileClu, dCentre,
-                        dDirMean, dDirConst, dDirLogNorm, dDirCov, dHostScoresT, dHostBestT, dMixOddMask};
+                        dDirMean, dDirConst, dDirLogNorm, dDirCov, dHostScoresT, dHostBestT, dMixOddMask,
+                        dPairMixOff, dPairCov, dPairQMean, dPairQConst, dPairFMean, dPairFConst, dPairLogNorm,
+                        dPairIsv};
         for (void* p : ptrs)
             if (p)
                 (void)hipFree(p);
+        if (hPairStage)
+            (void)hipHostFree(hPairStage);
         for (auto& kv : chunks)
             if (kv.second.dMixOff)
                 (void)hipFree(kv.second.dMixOff);
@@ -1211,6 +1230,51 @@ namespace {
 
 namespace {
 
+// gmm_best_density_pairs' entry-major tables (the assigning types): SIMD-diagonal-maximum the reference's prepared
+// u8 means and constant weights of the shard's entries (q: the scorer's own preparation, dIsv its isv * s rows);
+// diagonal-maximum / diagonal-sum the direct scorer's reference-order rows (prepareDirect).  A model the direct
+// layout does not take (D > 128) has no sparse path: gmm_best_density_pairs reports it, the caller refills.
+int setupPairs(gmm_scorer* s, const gmm_mixture_set& ms, ShardRange shard, const PreparedQuantized* q) {
+    if (shard.begin == 0 && shard.end == 0)
+        shard.end = ms.n_mixtures;
+    const uint32_t eb = ms.mixture_offsets[shard.begin], ee = ms.mixture_offsets[shard.end];
+    std::vector<uint32_t> mixOff(shard.end - shard.begin + 1), cov(ee - eb);
+    for (uint32_t m = shard.begin; m <= shard.end; ++m)
+        mixOff[m - shard.begin] = ms.mixture_offsets[m] - eb;
+    for (uint32_t e = eb; e < ee; ++e)
+        cov[e - eb] = ms.density_covariance[ms.mixture_densities[e]];
+    int rc = GMM_OK;
+    if (s->flavor == Flavor::Simd) {
+        if (!q)
+            return GMM_OK;
+        const size_t         Dp = q->paddedDimension;
+        std::vector<uint8_t> mean(q->preparedMean.begin() + eb * Dp, q->preparedMean.begin() + ee * Dp);
+        std::vector<int32_t> cst(q->constantWeight.begin() + eb, q->constantWeight.begin() + ee);
+        if ((rc = upload(&s->dPairQMean, mean)) || (rc = upload(&s->dPairQConst, cst)))
+            return rc;
+        s->pairIsvStride = q->kSteps * kI8K;  // dIsv: [C][kSteps * 64]
+        s->pairKind      = kPairSimd;
+    }
+    else if (s->flavor == Flavor::DiagonalMaximum || s->flavor == Flavor::DiagonalSum) {
+        PreparedDirect p;
+        const uint32_t nb = directBlocks(ms.dimension, false);
+        if (nb == 0 || !prepareDirect(ms, Flavor::DiagonalMaximum, s->cfg.mixture_weight_scale, s->cfg.gaussian_scale,
+                                      shard, nb, p).empty())
+            return GMM_OK;
+        if ((rc = upload(&s->dPairFMean, p.mean)) || (rc = upload(&s->dPairFConst, p.constant)) ||
+            (rc = upload(&s->dPairLogNorm, p.logNorm)) || (rc = upload(&s->dPairIsv, p.isv)))
+            return rc;
+        s->pairL    = p.L;
+        s->pairNb   = p.nb;
+        s->pairKind = s->flavor == Flavor::DiagonalSum ? kPairDiagonalSum : kPairDiagonalMaximum;
+    }
+    else
+        return GMM_OK;
+    if ((rc = upload(&s->dPairMixOff, mixOff)) || (rc = upload(&s->dPairCov, cov)))
+        s->pairKind = -1;
+    return rc;
+}
+
 // classLayout: lay the quantized model out for the score-only kernel (gmm_prepare.cc buildClassLayout) whatever
 // the type (the SIMD scorer's scoresOnly twin); batch-int/-fast use it by default
 int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scorer_config* config, int device,
@@ -1317,6 +1381,8 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
         if (presel && (rc = setupPreselection(s.get(), *ms, p.preparedMean.data(), p.paddedDimension,
                                               p.tiling.rowEntry, nullptr)) != GMM_OK)
             return rc;
+        if (!classLayout && (rc = setupPairs(s.get(), *ms, shard, &p)) != GMM_OK)
+            return rc;
     }
     else if (direct) {
         PreparedDirect p;
@@ -1332,7 +1398,7 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
         s->mixTileOff = p.mixOff;
         if ((rc = upload(&s->dDirMean, p.mean)) || (rc = upload(&s->dIsv, p.isv)) || (rc = upload(&s->dDirCov, p.entryCov)) ||
             (rc = upload(&s->dDirConst, p.constant)) || (rc = upload(&s->dDirLogNorm, p.logNorm)) ||
-            (rc = upload(&s->dMixTileOff, s->mixTileOff)))
+            (rc = upload(&s->dMixTileOff, s->mixTileOff)) || (rc = setupPairs(s.get(), *ms, shard, nullptr)))
             return rc;
     }
     else {
@@ -1386,6 +1452,8 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
                 if ((rc = setupPreselection(s.get(), *ms, em.data(), Dp, p.tiling.rowEntry, &p.splitFillEntry)) != GMM_OK)
                     return rc;
             }
+            if ((rc = setupPairs(s.get(), *ms, shard, nullptr)) != GMM_OK)
+                return rc;
             s->mixBase = shard.begin == 0 && shard.end == 0 ? 0 : shard.begin;
             GMM_HIP_CHECK(hipDeviceSynchronize());
             *out = s.release();
@@ -1402,6 +1470,8 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
         GMM_HIP_CHECK(hipMemset(s->dFrameX, 0, nX * s->kSteps * 4 * sizeof(float)));
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameXX), nX * sizeof(float)));
         GMM_HIP_CHECK(hipMemset(s->dFrameXX, 0, nX * sizeof(float)));
+        if ((rc = setupPairs(s.get(), *ms, shard, nullptr)) != GMM_OK)
+            return rc;
     }
     s->mixBase = shard.begin == 0 && shard.end == 0 ? 0 : shard.begin;
     GMM_HIP_CHECK(hipDeviceSynchronize());
@@ -1706,6 +1776,114 @@ int gmm_fetch_best_density(gmm_scorer* s, uint64_t callId, uint32_t* best, uint3
     if (rc != GMM_OK)
         (void)hipStreamSynchronize(s->hostCopy);
     return rc;
+}
+
+namespace {
+PairArgs pairArgsOf(const gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride) {
+    PairArgs a{};
+    a.frames      = frames;
+    a.nFrames     = nFrames;
+    a.frameStride = frameStride;
+    a.mixOff      = s->dPairMixOff;
+    a.entryCov    = s->dPairCov;
+    a.qMean       = s->dPairQMean;
+    a.qConst      = s->dPairQConst;
+    a.fMean       = s->dPairFMean;
+    a.fConst      = s->dPairFConst;
+    a.fLogNorm    = s->dPairLogNorm;
+    a.isv         = s->pairKind == kPairSimd ? s->dIsv : s->dPairIsv;
+    a.nMixtures   = s->nMix;
+    a.D           = s->D;
+    a.Dp          = s->paddedDimension;
+    a.L           = s->pairL;
+    a.nb          = s->pairNb;
+    a.isvStride   = s->pairIsvStride;
+    a.kind        = s->pairKind;
+    return a;
+}
+
+int checkPairs(const gmm_scorer* s) {
+    if (!hasAssignment(s))
+        return fail(GMM_ERR_UNSUPPORTED, "scorer type has no best densities (batch types)");
+    if (s->group || s->pairKind < 0)
+        return fail(GMM_ERR_UNSUPPORTED, "no sparse best-density path for this scorer (density-sharded handle, or a "
+                                         "float model of dimension > 128): use gmm_fetch_best_density");
+    return GMM_OK;
+}
+}  // namespace
+
+int gmm_best_density_pairs(gmm_scorer* s, uint64_t callId, const uint32_t* positions, const uint32_t* mixtures,
+                           uint32_t nPairs, uint32_t* best) {
+    if (!s || (nPairs && (!positions || !mixtures || !best)))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    const int wrc = waitAsync(s);
+    if (wrc != GMM_OK)
+        return wrc;
+    int rc = checkPairs(s);
+    if (rc != GMM_OK)
+        return rc;
+    if (callId == 0 || callId != s->keptBestCall)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "no frames kept for this call (a later host call replaced them)");
+    if (nPairs == 0)
+        return GMM_OK;
+    const HostRing& r = s->keptRing;
+    GMM_HIP_CHECK(hipSetDevice(s->device));
+    if (s->pairStageCap < nPairs) {
+        if (s->hPairStage)
+            GMM_HIP_CHECK(hipHostFree(s->hPairStage));
+        s->hPairStage   = nullptr;
+        s->pairStageCap = 0;
+        const size_t cap = std::max<size_t>(nPairs, 256);
+        GMM_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s->hPairStage), 3 * cap * sizeof(uint32_t),
+                                    hipHostMallocMapped));
+        s->pairStageCap = cap;
+    }
+    uint32_t* st = s->hPairStage;
+    for (uint32_t i = 0; i < nPairs; ++i) {
+        // ring position -> frame of the call (the call's frame t sits at ring position (first + t) % ringSize)
+        const uint32_t pos = positions[i];
+        const uint32_t t   = pos < r.ringSize ? (pos + r.ringSize - r.first) % r.ringSize : 0xffffffffu;
+        if (t >= r.nFrames)
+            return fail(GMM_ERR_INVALID_ARGUMENT, "position not scored by this call");
+        if (mixtures[i] >= s->nMix)
+            return fail(GMM_ERR_INVALID_ARGUMENT, "mixture index out of range");
+        st[i]          = t;
+        st[nPairs + i] = mixtures[i];
+    }
+    uint32_t* dst = nullptr;
+    GMM_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), st, 0));
+    PairArgs a  = pairArgsOf(s, s->dHostFrames, r.nFrames, s->D);
+    a.pairFrame = dst;
+    a.pairMix   = dst + nPairs;
+    a.best      = dst + 2 * static_cast<size_t>(nPairs);
+    a.nPairs    = nPairs;
+    // after the call's own frame staging on hostCompute (the kernel reads dHostFrames)
+    GMM_HIP_CHECK(launchBestPairs(a, s->hostCompute));
+    GMM_HIP_CHECK(hipStreamSynchronize(s->hostCompute));
+    std::memcpy(best, st + 2 * static_cast<size_t>(nPairs), nPairs * sizeof(uint32_t));
+    return GMM_OK;
+}
+
+int gmm_best_density_pairs_device(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t frameStride,
+                                  const uint32_t* pairFrame, const uint32_t* pairMixture, uint32_t nPairs,
+                                  uint32_t* best, void* stream) {
+    if (!s || (nPairs && (!frames || !pairFrame || !pairMixture || !best)))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    int rc = checkPairs(s);
+    if (rc != GMM_OK)
+        return rc;
+    if (frameStride < s->D)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "frame_stride below the dimension");
+    if (nPairs == 0)
+        return GMM_OK;
+    GMM_HIP_CHECK(hipSetDevice(s->device));
+    PairArgs a  = pairArgsOf(s, frames, nFrames, frameStride);
+    a.pairFrame = pairFrame;
+    a.pairMix   = pairMixture;
+    a.best      = best;
+    a.nPairs    = nPairs;
+    GMM_HIP_CHECK(launchBestPairs(a, static_cast<hipStream_t>(stream)));
+    return GMM_OK;
 }
 
 int gmm_host_alloc(size_t bytes, void** ptr) {

@@ -187,6 +187,30 @@ struct DirectArgs {
 };
 hipError_t launchScoreDirect(const DirectArgs& a, hipStream_t stream);
 uint32_t   directBlocks(uint32_t D, bool batch);  // 4-dimension blocks of the row layout, 0 = unsupported
+
+// sparse best densities (gmm_best_density_pairs, gmm_kernels_pairs.hip): one wave per (frame, mixture) pair,
+// the mixture's entries scored in the reference's own arithmetic and scanned in entry order
+enum PairKind : int { kPairSimd = 0, kPairDiagonalMaximum = 1, kPairDiagonalSum = 2 };
+struct PairArgs {
+    const float*    frames;      // [nFrames][frameStride]
+    const uint32_t* pairFrame;   // [nPairs] frame of the pair
+    const uint32_t* pairMix;     // [nPairs] mixture of the pair (shard-relative)
+    uint32_t*       best;        // [nPairs] density in mixture, 0xffffffff: none (empty mixture, no finite score)
+    const uint32_t* mixOff;      // [nMixtures+1] entry offsets (shard-relative)
+    const uint32_t* entryCov;    // [entries]
+    // SIMD-diagonal-maximum: prepared means (u8, rows of Dp), constant weights, isv * s rows of isvStride
+    const uint8_t*  qMean;
+    const int32_t*  qConst;
+    // diagonal-maximum / diagonal-sum: the reference-order row layout of the direct scorer (rows of L floats)
+    const float*    fMean;
+    const float*    fConst;      // minus2LogWeights
+    const float*    fLogNorm;    // [C]
+    const float*    isv;         // SIMD: [C][isvStride]; float: [C][L]
+    uint32_t        nFrames, frameStride, nPairs, nMixtures;
+    uint32_t        D, Dp, L, nb, isvStride;
+    int             kind;        // PairKind
+};
+hipError_t launchBestPairs(const PairArgs& a, hipStream_t stream);
 // quantized LDS kernel: the never-winning stand-in tile after the segment ring (operands, row constants,
 // PRESEL cluster offsets)
 constexpr uint32_t kI8DummyTileBytes(int ks, bool presel) { return static_cast<uint32_t>(ks) * 1024u + 64u + (presel ? 64u : 0u); }

@@ -233,16 +233,25 @@ public:
         return row_[e];
     }
     bool             hasBestDensity() const override { return assigning_; }
+    // the position's best-density row once its call carried one (the same generation check as score(e)); a
+    // position of a score-only call answers through getBestDensity (one pair, or the call's whole table)
     DensityInMixture bestDensity(EmissionIndex e) const override {
-        return parent_->getBestDensity(e, currentFeature_, buffered_);
+        const uint32_t g = parent_->positionGeneration(currentFeature_);
+        if (!bestRow_ || g != bestGen_) {
+            bestRow_ = parent_->bestRow(currentFeature_, buffered_);
+            bestGen_ = g;
+        }
+        return bestRow_ ? bestRow_[e] : parent_->getBestDensity(e, currentFeature_, buffered_);
     }
 
 private:
-    const GpuBatchFeatureScorer* parent_;
-    uint32_t                     currentFeature_, buffered_;
-    bool                         assigning_;
-    mutable const float*         row_ = nullptr;
-    mutable uint32_t             gen_ = 0;
+    const GpuBatchFeatureScorer*    parent_;
+    uint32_t                        currentFeature_, buffered_;
+    bool                            assigning_;
+    mutable const float*            row_ = nullptr;
+    mutable uint32_t                gen_ = 0;
+    mutable const DensityInMixture* bestRow_ = nullptr;
+    mutable uint32_t                bestGen_ = 0;
 };
 
 }  // namespace
@@ -258,6 +267,8 @@ struct GpuFeatureScorer::Slot {
     std::vector<float>  scratch; // scores of that second scoring (the context keeps its first ones)
     uint64_t            call = 0;
     bool                bestValid = false;
+    // bestDensity(e) of a score-only call answered one emission at a time (gmm_best_density_pairs)
+    std::vector<std::pair<EmissionIndex, DensityInMixture>> sparse;
 };
 
 struct GpuFeatureScorer::SlotPool {
@@ -300,15 +311,30 @@ Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
     }
     std::copy(f.begin(), f.end(), slot->frame.data());
     ++launches_;
-    if (gmm_score_host_ring(handle_, slot->frame.data(), 1, 0, 1, dimension_, slot->scores.data(), nullptr, 1,
-                            assigning_ ? GMM_HOST_LAZY_BEST : 0u, &slot->call) != GMM_OK)
+    // an aligner (bestDensity() was asked before): the best densities come with the scores, in the same launch
+    const bool eager = assigning_ && bestEager_;
+    if (gmm_score_host_ring(handle_, slot->frame.data(), 1, 0, 1, dimension_, slot->scores.data(),
+                            eager ? slot->best.data() : nullptr, 1, (assigning_ && !eager) ? GMM_HOST_LAZY_BEST : 0u,
+                            &slot->call) != GMM_OK)
         criticalError("gmm_score_host_ring");
-    slot->bestValid = false;
+    slot->bestValid = eager;
+    slot->sparse.clear();
     return std::make_shared<FrameScorer>(this, std::move(slot), pool_, nMixtures_, assigning_);
 }
 
 DensityInMixture GpuFeatureScorer::slotBestDensity(Slot& slot, EmissionIndex e) const {
+    bestEager_ = true;  // from the next getScorer() on, the calls compute best densities too
     if (!slot.bestValid) {
+        // the asked emission alone, while the frame is still on the device (its call is the newest)
+        for (const auto& kv : slot.sparse)
+            if (kv.first == e)
+                return kv.second;
+        uint32_t pos = 0, v = 0;
+        if (slot.sparse.size() < kSparseMax && gmm_best_density_pairs(handle_, slot.call, &pos, &e, 1, &v) == GMM_OK) {
+            ++bestPairs_;
+            slot.sparse.emplace_back(e, v);
+            return v;
+        }
         // computed from the frame the device still holds if no later frame was scored; otherwise score this
         // frame again, its best densities copied directly (its scores into scratch: the float types' keyed
         // scores carry fewer bits, and the context's scores stay the ones it already returned)
@@ -376,7 +402,7 @@ void GpuBatchFeatureScorer::setFeature(size_t pos, const FeatureVector& f) const
         landInflight();
     std::copy(f.begin(), f.end(), features_.data() + pos * dimension_);
     ++generation_[pos];
-    if (!prefetchChunk_ || bestWanted_)
+    if (!prefetchChunk_)
         return;
     // the new frame joins the pending run (it is the newest buffered position)
     if (pendingCount_ == 0)
@@ -399,7 +425,7 @@ void GpuBatchFeatureScorer::landInflight() const {
         if (inflight_[q]) {
             inflight_[q]   = 0;
             cached_[q]     = 1;
-            bestCached_[q] = 0;
+            bestCached_[q] = asyncEager_ ? 1 : 0;
             bestCall_[q]   = asyncCall_;
         }
     asyncCall_ = 0;
@@ -407,12 +433,15 @@ void GpuBatchFeatureScorer::landInflight() const {
 
 void GpuBatchFeatureScorer::submitPending() const {
     landInflight();  // one call in flight at a time (the library's staging)
-    uint64_t call = 0;
+    uint64_t   call  = 0;
+    const bool eager = assigning_ && bestEager_;
     ++launches_;
     if (gmm_score_host_ring(handle_, features_.data(), bufferSize_, pendingFirst_, pendingCount_, dimension_, scores_.data(),
-                            nullptr, rowStride(),
-                            GMM_HOST_FRAME_MAJOR | GMM_HOST_ASYNC | (assigning_ ? GMM_HOST_LAZY_BEST : 0u), &call) != GMM_OK)
+                            eager ? best_.data() : nullptr, rowStride(),
+                            GMM_HOST_FRAME_MAJOR | GMM_HOST_ASYNC | ((assigning_ && !eager) ? GMM_HOST_LAZY_BEST : 0u),
+                            &call) != GMM_OK)
         criticalError("gmm_score_host_ring");
+    asyncEager_ = eager;
     for (uint32_t i = 0; i < pendingCount_; ++i) {
         const uint32_t q = (pendingFirst_ + i) % bufferSize_;
         inflight_[q]     = 1;
@@ -458,21 +487,23 @@ Scorer GpuBatchFeatureScorer::flush() const {
 // and cache them (the reference's fillScoreCache does one mixture at a time): one gmm_score_host_ring call
 // reads those rows of features_ and writes their rows of the page-locked frame-major tables in place,
 // wrapped or not.
-void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length) const {
+void GpuBatchFeatureScorer::fill(uint32_t featureIndex, uint32_t length, bool withBest) const {
     const uint32_t b = bufferSize_;
     length           = std::min(length, b);
     const uint32_t p = featureIndex % b;
-    uint64_t       call = 0;
+    uint64_t       call  = 0;
+    const bool     eager = assigning_ && withBest;
     landInflight();
     pendingCount_ = 0;  // this fill covers every buffered position from p on
     ++launches_;
-    if (gmm_score_host_ring(handle_, features_.data(), b, p, length, dimension_, scores_.data(), nullptr, rowStride(),
-                            GMM_HOST_FRAME_MAJOR | (assigning_ ? GMM_HOST_LAZY_BEST : 0u), &call) != GMM_OK)
+    if (gmm_score_host_ring(handle_, features_.data(), b, p, length, dimension_, scores_.data(),
+                            eager ? best_.data() : nullptr, rowStride(),
+                            GMM_HOST_FRAME_MAJOR | ((assigning_ && !eager) ? GMM_HOST_LAZY_BEST : 0u), &call) != GMM_OK)
         criticalError("gmm_score_host_ring");
     for (uint32_t i = 0; i < length; ++i) {
         const uint32_t q = (p + i) % b;
         cached_[q]       = 1;
-        bestCached_[q]   = 0;
+        bestCached_[q]   = eager ? 1 : 0;
         bestCall_[q]     = call;
     }
 }
@@ -488,54 +519,72 @@ const float* GpuBatchFeatureScorer::scoreRow(uint32_t featureIndex, uint32_t len
     if (!cached_[p] && inflight_[p])
         landInflight();
     if (!cached_[p])
-        fill(featureIndex, length);
+        fill(featureIndex, length, bestEager_);
     return scores_.data() + static_cast<size_t>(p) * rowStride();
+}
+
+const DensityInMixture* GpuBatchFeatureScorer::bestRow(uint32_t featureIndex, uint32_t length) const {
+    if (!assigning_)
+        return nullptr;
+    bestEager_       = true;
+    const uint32_t p = featureIndex % bufferSize_;
+    if (!cached_[p] && inflight_[p])
+        landInflight();
+    if (!cached_[p])
+        fill(featureIndex, length, true);
+    return bestCached_[p] ? best_.data() + static_cast<size_t>(p) * rowStride() : nullptr;
 }
 
 DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {
     assert(e < nMixtures_);
     if (!assigning_)
         return 0xffffffffu;
-    bestWanted_      = true;  // an aligner: no more prefetch (its calls' best densities would not stay kept)
+    bestEager_       = true;  // an aligner: from now on every call computes the best densities with the scores
     const uint32_t p = featureIndex % bufferSize_;
     if (!cached_[p] && inflight_[p])
         landInflight();
     if (!cached_[p])
-        fill(featureIndex, length);
-    if (!bestCached_[p]) {
-        const uint64_t call = bestCall_[p];
-        if (gmm_fetch_best_density(handle_, call, best_.data(), rowStride()) == GMM_OK) {
-            ++bestFetches_;  // every position of that call
-            for (uint32_t q = 0; q < bufferSize_; ++q)
-                if (cached_[q] && bestCall_[q] == call)
-                    bestCached_[q] = 1;
-        }
-        else if (fill(featureIndex, length),
-                 gmm_fetch_best_density(handle_, bestCall_[p], best_.data(), rowStride()) == GMM_OK) {
-            // a later call replaced its frames on the device (e.g. a prefetch before the first bestDensity()):
-            // the buffered positions from p scored again in one call (the same score-only values), their best
-            // densities computed from it
-            ++bestFetches_;
-            const uint64_t refill = bestCall_[p];
-            for (uint32_t q = 0; q < bufferSize_; ++q)
-                if (cached_[q] && bestCall_[q] == refill)
-                    bestCached_[q] = 1;
-        }
-        else {
-            // (not reached with this library: the fill above is the newest call) score this position again,
-            // best densities copied directly into its row of best_, the scores into scratch
-            uint64_t again = 0;
-            ++launches_;
-            scratch_.resize(rowStride());
-            if (gmm_score_host_ring(handle_, features_.data() + static_cast<size_t>(p) * dimension_, 1, 0, 1, dimension_,
-                                    scratch_.data(), best_.data() + static_cast<size_t>(p) * rowStride(), rowStride(),
-                                    GMM_HOST_FRAME_MAJOR, &again) != GMM_OK)
-                criticalError("gmm_score_host_ring");
-            bestCall_[p] = again;
-        }
-        bestCached_[p] = 1;
+        fill(featureIndex, length, true);
+    const size_t o = static_cast<size_t>(p) * rowStride() + e;
+    if (bestCached_[p])
+        return best_[o];
+    // a position of a score-only call (made before the first bestDensity()): the asked pair alone while that
+    // call's asked set is small and its frames are still on the device
+    const uint64_t call = bestCall_[p];
+    if (call != sparseCall_) {
+        sparseCall_  = call;
+        sparseAsked_ = 0;
+        sparse_.clear();
     }
-    return best_[static_cast<size_t>(p) * rowStride() + e];
+    const uint64_t key = (static_cast<uint64_t>(p) << 32) | e;
+    const auto     it  = sparse_.find(key);
+    if (it != sparse_.end())
+        return it->second;
+    if (sparseAsked_ < kSparseMax) {
+        uint32_t pos = p, v = 0;
+        if (gmm_best_density_pairs(handle_, call, &pos, &e, 1, &v) == GMM_OK) {
+            ++sparseAsked_;
+            ++bestPairs_;
+            sparse_.emplace(key, v);
+            return v;
+        }
+    }
+    // past kSparseMax pairs: the call's whole table, computed from its frames on the device (every position of the
+    // call); if a later call replaced them (a prefetch before the first bestDensity()), the buffered positions from
+    // p are scored again, scores only (the values the contexts already returned), and their table computed from it
+    bool ok = gmm_fetch_best_density(handle_, call, best_.data(), rowStride()) == GMM_OK;
+    if (!ok) {
+        fill(featureIndex, length, false);
+        ok = gmm_fetch_best_density(handle_, bestCall_[p], best_.data(), rowStride()) == GMM_OK;
+    }
+    if (!ok)  // (not reached with this library: the fill above is the newest call)
+        criticalError("gmm_fetch_best_density");
+    ++bestFetches_;
+    const uint64_t filled = bestCall_[p];
+    for (uint32_t q = 0; q < bufferSize_; ++q)
+        if (cached_[q] && bestCall_[q] == filled)
+            bestCached_[q] = 1;
+    return best_[o];
 }
 
 // ---------------------------------------------------------------------------

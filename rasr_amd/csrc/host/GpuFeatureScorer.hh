@@ -18,6 +18,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -171,9 +172,12 @@ protected:
 
 // Unbuffered scorer: every getScorer() scores one frame against all mixtures on the GPU
 // (the SIMD / diagonal-maximum scorers' Context, SimdFeatureScorer.cc:22-35).  The contexts' tables are
-// page-locked slots recycled when the caller drops a context (no allocation per frame); best densities
-// are computed only when bestDensity() asks for them (GMM_HOST_LAZY_BEST + gmm_fetch_best_density from the
-// frame still on the device), or -- after a later frame replaced it there -- that frame is scored again.  Contexts refer to their scorer, which must
+// page-locked slots recycled when the caller drops a context (no allocation per frame).  Best densities:
+// until the first bestDensity() the calls compute scores only (GMM_HOST_LAZY_BEST), and a context's
+// bestDensity(e) is answered for that one emission (gmm_best_density_pairs, from the frame still on the device;
+// past kSparseMax emissions of a context its whole table, gmm_fetch_best_density), or -- after a later frame
+// replaced it there -- by scoring that frame again.  From the first bestDensity() on (an aligner) every call
+// computes the best densities with the scores, in the same launch.  Contexts refer to their scorer, which must
 // outlive them (as the reference's Context refers to its featureScorer_, SimdFeatureScorer.hh:51-68).
 class GpuFeatureScorer : public FeatureScorer {
 public:
@@ -188,13 +192,18 @@ public:
     // host calls so far (tests: bestDensity() of the newest context copies, an older one re-scores)
     uint32_t nLaunches() const { return launches_; }
     uint32_t nBestFetches() const { return bestFetches_; }
+    uint32_t nBestPairs() const { return bestPairs_; }  // bestDensity(e) answered by gmm_best_density_pairs
     // bestDensity of a context whose slot is `slot` (ContextScorer side)
     DensityInMixture slotBestDensity(Slot& slot, EmissionIndex e) const;
+
+    // emissions of one score-only call answered one by one before its whole table is computed
+    static constexpr uint32_t kSparseMax = 32;
 
 private:
     GpuFeatureScorer() {}
     std::shared_ptr<SlotPool> pool_;
-    mutable uint32_t          launches_ = 0, bestFetches_ = 0;
+    mutable bool              bestEager_ = false;  // a bestDensity() was asked: calls compute best densities too
+    mutable uint32_t          launches_ = 0, bestFetches_ = 0, bestPairs_ = 0;
 };
 
 // Buffered scorer: the BatchFeatureScorerBase ring-buffer protocol (BatchFeatureScorer.cc:40-116).
@@ -224,15 +233,23 @@ public:
     uint32_t         positionGeneration(uint32_t featureIndex) const { return generation_[featureIndex % bufferSize_]; }
     // 0xffffffff for the batch types, which have no assignment (as ContextScorer::bestDensity)
     DensityInMixture getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
+    // the best densities of every emission of the position (filled first if needed, with best densities), or NULL
+    // while they are not in the table (a score-only call's position: getBestDensity answers); valid as scoreRow()
+    const DensityInMixture* bestRow(uint32_t featureIndex, uint32_t length) const;
 
     // number of GPU launches so far (tests check that one launch serves a whole buffer, wrapped or not)
     uint32_t nLaunches() const { return launches_; }
     uint32_t nBestFetches() const { return bestFetches_; }
+    uint32_t nBestPairs() const { return bestPairs_; }  // bestDensity(e) answered by gmm_best_density_pairs
+
+    // (position, emission) pairs of one score-only call answered one by one before its whole table is computed
+    static constexpr uint32_t kSparseMax = 32;
 
 private:
     GpuBatchFeatureScorer() {}
     void     setFeature(size_t pos, const FeatureVector& f) const;
-    void     fill(uint32_t featureIndex, uint32_t length) const;
+    // withBest: the call computes the best densities too (bestEager_), else scores only (GMM_HOST_LAZY_BEST)
+    void     fill(uint32_t featureIndex, uint32_t length, bool withBest) const;
     void     submitPending() const;   // the pending run as a GMM_HOST_ASYNC call
     void     landInflight() const;    // wait for the asynchronous call; its positions become cached
     uint32_t rowStride() const { return nMixtures_ ? nMixtures_ : 1; }
@@ -243,13 +260,15 @@ private:
     // positions, wrapped or not, whose frames and score rows move by DMA directly.  The tables are
     // frame-major, [bufferSize][nMixtures] (the reference's scores_ is [nMixtures][bufferSize],
     // BatchFeatureScorer.hh:177-186, filled one mixture at a time): a context's score(e) calls walk one
-    // contiguous row instead of one cache line per emission.  Best densities (assigning types) are
-    // computed only when bestDensity() asks for them (GMM_HOST_LAZY_BEST): a score-only caller runs the
-    // score-only kernels and moves 4 B per (frame, mixture), not 8.
+    // contiguous row instead of one cache line per emission.  Best densities (assigning types): until the
+    // first bestDensity() the calls compute scores only (GMM_HOST_LAZY_BEST) -- a score-only caller (the
+    // search) runs the score-only kernels and moves 4 B per (frame, mixture), not 8 -- and the positions of
+    // such a call answer bestDensity(e) one pair at a time (gmm_best_density_pairs) up to kSparseMax pairs,
+    // then from the call's whole table (gmm_fetch_best_density).  From the first bestDensity() on (an
+    // aligner, a dump) every call, prefetches included, writes the best table with the scores (bestEager_).
     HostTable<float>          features_;
     HostTable<float>          scores_;
     HostTable<uint32_t>       best_;
-    mutable std::vector<float> scratch_;     // [nMixtures] scores of a re-scored position (not kept)
     mutable std::vector<char> cached_;       // [bufferSize] scores of the position are in scores_
     mutable std::vector<uint32_t> generation_; // [bufferSize] frames the position has taken (positionGeneration)
     mutable std::vector<char> bestCached_;   // [bufferSize] best densities of the position are in best_
@@ -257,17 +276,21 @@ private:
     // Prefetch (buffers of kPrefetchMin frames and more): the newest frames not yet scored (pending: the ring run
     // [pendingFirst_, pendingFirst_ + pendingCount_)) go to the GPU as one GMM_HOST_ASYNC call once they number
     // prefetchChunk_ (half the ring), so the GPU scores them while the caller still consumes older positions; a position whose
-    // score is asked for while its call is in flight waits for it (inflight_).  Off once bestDensity() was asked
-    // for (the aligners' best densities are fetched from the newest call only).
+    // score is asked for while its call is in flight waits for it (inflight_).
     static constexpr uint32_t kPrefetchMin = 64;
     uint32_t                  prefetchChunk_ = 0;  // 0: no prefetch
     mutable std::vector<char> inflight_;           // [bufferSize] scored by asyncCall_, not landed yet
     mutable uint64_t          asyncCall_    = 0;
     mutable uint32_t          pendingFirst_ = 0, pendingCount_ = 0;
-    mutable bool              bestWanted_   = false;
+    mutable bool              bestEager_    = false;  // a bestDensity() was asked: calls compute best densities
+    mutable bool              asyncEager_   = false;  // the call in flight does
+    // the score-only call whose pairs were answered one by one, how many, and the answers (key position << 32 | e)
+    mutable uint64_t          sparseCall_ = 0;
+    mutable uint32_t          sparseAsked_ = 0;
+    mutable std::unordered_map<uint64_t, DensityInMixture> sparse_;
     mutable int32_t           currentFeature_ = 0;
     mutable int32_t           buffered_       = 0;
-    mutable uint32_t          launches_       = 0, bestFetches_ = 0;
+    mutable uint32_t          launches_       = 0, bestFetches_ = 0, bestPairs_ = 0;
 };
 
 // Factory by reference type name ("SIMD-diagonal-maximum", "diagonal-maximum",

@@ -213,6 +213,36 @@ class Scorer:
         _capi.check(self._lib.gmm_fetch_best_density(self._h, int(call_id), best_out.ctypes.data_as(ctypes.c_void_p),
                                                      best_out.shape[1]), "gmm_fetch_best_density")
 
+    def best_pairs(self, call_id: int, positions, mixtures) -> np.ndarray:
+        """gmm_best_density_pairs: best densities of (ring position, mixture) pairs of host call `call_id` (made with
+        keep_best or lazy_best), from its frames still on the device."""
+        pos = np.ascontiguousarray(positions, dtype=np.uint32)
+        mix = np.ascontiguousarray(mixtures, dtype=np.uint32)
+        if pos.shape != mix.shape or pos.ndim != 1:
+            raise ValueError("positions and mixtures must be 1-d arrays of one length")
+        out = np.empty(pos.shape[0], dtype=np.uint32)
+        _capi.check(self._lib.gmm_best_density_pairs(self._h, int(call_id), pos.ctypes.data_as(ctypes.c_void_p),
+                                                     mix.ctypes.data_as(ctypes.c_void_p), pos.shape[0],
+                                                     out.ctypes.data_as(ctypes.c_void_p)), "gmm_best_density_pairs")
+        return out
+
+    def best_pairs_device(self, frames, pair_frame, pair_mixture, out, stream=None, n_frames=None) -> None:
+        """gmm_best_density_pairs_device: frames torch cuda f32 [F, >=D]; pair_frame / pair_mixture / out: int32 or
+        uint32 cuda tensors of n_pairs.  Asynchronous on `stream`."""
+        f = int(frames.shape[0] if n_frames is None else n_frames)
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device)
+        s = getattr(stream, "cuda_stream", stream)
+        n = int(pair_frame.numel())
+        if pair_mixture.numel() != n or out.numel() < n:
+            raise ValueError("pair_frame, pair_mixture and out must hold n_pairs entries")
+        rc = self._lib.gmm_best_density_pairs_device(self._h, ctypes.c_void_p(frames.data_ptr()), f, int(frames.stride(0)),
+                                                     ctypes.c_void_p(pair_frame.data_ptr()),
+                                                     ctypes.c_void_p(pair_mixture.data_ptr()), n,
+                                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s) if s else None)
+        _capi.check(rc, "gmm_best_density_pairs_device")
+
     def set_timing(self, enable: bool) -> None:
         _capi.check(self._lib.gmm_scorer_set_timing(self._h, int(bool(enable))), "gmm_scorer_set_timing")
 

@@ -72,7 +72,8 @@ static std::unique_ptr<Mm::Gpu::MixtureSet> readBinaryModel(const std::string& p
 // bufferSizes / frames: comma-separated lists of equal length (one scorer per buffer size, timed on that many
 // frames).  Synthetic model of SURVEY 8(d) (means N(0,1), pooled variance 0.5 + |N(0,1)|, uniform weights;
 // splitmix64 + Box-Muller) and N(0,1) frames.  Every frame's context is consumed as FeatureScorerNode dumps
-// it: score(e) for every emission (and bestDensity(e) for every emission with best = 1, the aligners' read).
+// it: score(e) for every emission (and bestDensity(e) for every emission with best = 1, the dump's read; with
+// best = 2 an aligner's read instead: bestDensity(e) of 1-10 emissions per frame, drawn per frame).
 // readPermille < 1000: a search-like consumer instead, score(e) of that share of the emissions per frame, a
 // scattered set that moves from frame to frame (the search's active states; SearchSpace.cc:1613-1659).
 // One warm-up segment, then one timed segment per size; prints one JSON line per size.
@@ -116,7 +117,8 @@ static int benchMain(int argc, char** argv) {
     const std::string           type  = argv[2];
     const std::vector<uint32_t> sizes = parseList(argv[3]), counts = parseList(argv[4]);
     const uint32_t              M = atoi(argv[5]), K = atoi(argv[6]), D = atoi(argv[7]);
-    const bool                  readBest = atoi(argv[8]) != 0;
+    const uint32_t              bestMode = static_cast<uint32_t>(atoi(argv[8]));
+    const bool                  readBest = bestMode != 0;
     if (sizes.empty() || sizes.size() != counts.size())
         return 2;
     Rng                 rng{12345};
@@ -167,6 +169,7 @@ static int benchMain(int argc, char** argv) {
                         a.push_back(e);
         }
         uint32_t frameNo = 0;
+        Rng      pick{999};
         auto     consume = [&](const Mm::Gpu::Scorer& s) {
             const uint32_t n   = s->nEmissions();
             float          acc = 0;
@@ -177,9 +180,14 @@ static int benchMain(int argc, char** argv) {
                 for (uint32_t e : active[frameNo++ & 63u])
                     acc += s->score(e);
             sink += acc;
-            if (readBest && s->hasBestDensity())
-                for (uint32_t e = 0; e < n; ++e)
-                    sinkB += s->bestDensity(e);
+            if (readBest && s->hasBestDensity()) {
+                if (bestMode == 2)  // an aligner: the frame's 1-10 aligned / competing emissions
+                    for (uint32_t k = 1 + static_cast<uint32_t>(pick.next() % 10u); k > 0; --k)
+                        sinkB += s->bestDensity(static_cast<uint32_t>(pick.next() % n));
+                else
+                    for (uint32_t e = 0; e < n; ++e)
+                        sinkB += s->bestDensity(e);
+            }
         };
         auto segment = [&](uint32_t t0, uint32_t t1) {
             scorer->reset();
@@ -208,7 +216,8 @@ static int benchMain(int argc, char** argv) {
         printf("{\"type\": \"%s\", \"buffer_size\": %u, \"frames\": %u, \"seconds\": %.6f, \"frames_per_s\": %.1f, "
                "\"launches\": %u, \"best\": %s, \"read_permille\": %u, \"mixtures\": %u, \"densities\": %u, "
                "\"dim\": %u, \"checksum\": %.6e}\n",
-               type.c_str(), B, F, sec, F / sec, lc() - l0, readBest ? "true" : "false", permille, M, M * K, D,
+               type.c_str(), B, F, sec, F / sec, lc() - l0, bestMode == 2 ? "\"sparse 1-10 per frame\"" : readBest ? "true" : "false",
+               permille, M, M * K, D,
                sink + double(sinkB));
         fflush(stdout);
     }
@@ -219,16 +228,19 @@ int main(int argc, char** argv) {
     if (argc >= 2 && std::string(argv[1]) == "bench")
         return benchMain(argc, argv);
     if (argc != 7 && argc != 8) {
-        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node|delayed|search|late]\n",
+        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node|delayed|search|late|aligner]\n",
                 argv[0]);
         return 2;
     }
     const std::string protocol = argc == 8 ? argv[7] : "recognizer";
     if (protocol != "recognizer" && protocol != "node" && protocol != "delayed" && protocol != "search" &&
-        protocol != "late")
+        protocol != "late" && protocol != "aligner")
         return 2;
     const bool search = protocol == "search";  // the recognizer's sequence, score(e) only (no bestDensity)
     const bool late   = protocol == "late";    // score(e) only for the first half of the frames, then bestDensity too
+    // an aligner's read (AbstractMixtureSetEstimator.cc:370-384): score(e) of every emission, bestDensity(e) of 1-10
+    // emissions per frame drawn from the frame's number (the others' best densities stay 0xffffffff in the output)
+    const bool aligner = protocol == "aligner";
     uint32_t   consumed = 0;
     const bool     delayed = protocol == "delayed";
     const uint32_t kDelay  = 3;
@@ -286,11 +298,19 @@ int main(int argc, char** argv) {
     auto consume = [&](const Mm::Gpu::Scorer& s) {  // the search reads score(e) for active e
         const uint32_t n        = node ? s->nEmissions() : M;  // the node dumps nEmissions() values per frame
         const bool     readBest = !search && (!late || 2 * consumed >= F) && s->hasBestDensity();
-        ++consumed;
+        const size_t   row      = outB.size();
         for (uint32_t e = 0; e < n; ++e) {
             outS.push_back(node ? -s->score(e) : s->score(e));  // FeatureScorerNode::putData: +log space
-            outB.push_back(readBest ? s->bestDensity(e) : 0xffffffffu);
+            outB.push_back(readBest && !aligner ? s->bestDensity(e) : 0xffffffffu);
         }
+        if (aligner && readBest) {
+            Rng pick{0x5eedull + consumed};
+            for (uint32_t k = 1 + static_cast<uint32_t>(pick.next() % 10u); k > 0; --k) {
+                const uint32_t e = static_cast<uint32_t>(pick.next() % n);
+                outB[row + e]    = s->bestDensity(e);
+            }
+        }
+        ++consumed;
     };
     const uint32_t segments = static_cast<uint32_t>(atoi(argv[6]));
     for (uint32_t seg = 0; seg < segments; ++seg) {

@@ -221,6 +221,29 @@ int gmm_fetch_best_density(gmm_scorer* s, uint64_t callId, uint32_t* best, uint3
     return GMM_OK;
 }
 
+int gmm_best_density_pairs(gmm_scorer* s, uint64_t callId, const uint32_t* positions, const uint32_t* mixtures,
+                           uint32_t nPairs, uint32_t* best) {
+    if (!s || (nPairs && (!positions || !mixtures || !best)))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    if (callId == 0 || callId != s->keptCall)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "no frames kept for this call");
+    const uint32_t n = static_cast<uint32_t>(s->keptPos.size());
+    for (uint32_t j = 0; j < nPairs; ++j) {
+        uint32_t i = 0;
+        while (i < n && s->keptPos[i] != positions[j])
+            ++i;
+        if (i == n || mixtures[j] >= s->M)
+            return fail(GMM_ERR_INVALID_ARGUMENT, "position not scored by this call or mixture out of range");
+        best[j] = s->kept[static_cast<size_t>(mixtures[j]) * n + i];
+    }
+    return GMM_OK;
+}
+
+int gmm_best_density_pairs_device(gmm_scorer*, const float*, uint32_t, uint32_t, const uint32_t*, const uint32_t*,
+                                  uint32_t, uint32_t*, void*) {
+    return fail(GMM_ERR_UNSUPPORTED, "stand-in: no device memory");
+}
+
 int gmm_host_alloc(size_t bytes, void** p) {
     if (!p)
         return fail(GMM_ERR_INVALID_ARGUMENT, "null ptr");

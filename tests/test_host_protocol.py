@@ -191,10 +191,10 @@ def test_protocol_model_from_estimator_file(gpu, tmp_path, kind):
 @pytest.mark.parametrize("kind", ["SIMD-diagonal-maximum", "diagonal-maximum"])
 def test_delayed_consumer_unbuffered(gpu, tmp_path, kind):
     """A consumer that reads each context only after 3 more frames were scored (RecognizerDelayHandler,
-    src/Speech/DelayedRecognizer.cc:65-135): scores come from the context's own page-locked slot, and its best
-    densities -- replaced on the device by the later frames (or by the re-scoring of an older context, which
-    is itself a host call) -- come from scoring its frame again: every frame is scored twice (launches = 2F).
-    The buffered protocol of test_simd_protocol_bit_exact covers the copy-on-demand path."""
+    src/Speech/DelayedRecognizer.cc:65-135): scores come from the context's own page-locked slot.  The first four
+    contexts were scored before any bestDensity() (scores only); their frames were replaced on the device by the
+    later ones, so their best densities come from scoring each frame again (4 launches).  From the first
+    bestDensity() on every getScorer() computes the best densities in its own launch (launches = F + 4)."""
     ms = ra.synthetic_mixture_set(30, 9, 39, seed=52, weights="random")
     frames = ra.synthetic_frames(29, 39, seed=53)
     s, b, launches = _run(tmp_path, ms, frames, kind, 1, 2, protocol="delayed")
@@ -205,7 +205,7 @@ def test_delayed_consumer_unbuffered(gpu, tmp_path, kind):
     else:
         ref_s, ref_b = oracle.OracleFloat(ms).score(frames)[:2]
         assert (np.abs(s.T.astype(np.float64) - ref_s) / np.maximum(1, np.abs(ref_s))).max() <= 1e-4
-    assert launches == 2 * 29
+    assert launches == 29 + 4
 
 
 @pytest.mark.gpu
@@ -242,7 +242,8 @@ def test_prefetch_search_protocol(gpu, tmp_path, kind, buffer_size):
 @pytest.mark.parametrize("protocol", ["recognizer", "node"])
 def test_prefetch_then_best_densities(gpu, tmp_path, protocol):
     """A buffer that prefetches, read by a consumer that asks bestDensity(e) too (the aligners; the node's dump):
-    prefetch stops at the first bestDensity(), the scores and best densities stay bit-exact."""
+    from the first bestDensity() on the prefetched calls carry the best densities too; the scores and best densities
+    stay bit-exact."""
     ms = ra.synthetic_mixture_set(30, 9, 39, seed=63, weights="random")
     frames = ra.synthetic_frames(260, 39, seed=64)
     s, b, _ = _run(tmp_path, ms, frames, "SIMD-diagonal-maximum", 64, 2, protocol=protocol)
@@ -272,3 +273,45 @@ def test_prefetch_then_late_best_densities(gpu, tmp_path, kind):
     assert (b[: F // 2] == 0xFFFFFFFF).all()
     agree = (b.T[:, F // 2:] == ref_b[:, F // 2:]).mean()
     assert agree == 1.0 if kind == "SIMD-diagonal-maximum" else agree > 0.99
+
+
+def _near_tie_ok(ms, frames, b, ref_b, asked):
+    """Float types: every asked best density equals the restatement's, or the two densities' scores (f64 here) are
+    within the float contract (1e-4 relative) -- a near tie either may name."""
+    t, e = np.nonzero(asked & (b != ref_b.T))
+    for ti, ei in zip(t, e):
+        lo = int(ms.mixture_offsets[ei])
+        sc = []
+        for d in (int(b[ti, ei]), int(ref_b[ei, ti])):
+            dns = ms.mixture_densities[lo + d]
+            var = ms.variances[ms.density_covariance[dns]].astype(np.float64)
+            dist = (((frames[ti] - ms.means[ms.density_mean[dns]]) / np.sqrt(var)) ** 2).sum()
+            sc.append(-2.0 * ms.mixture_log_weights[lo + d] + oracle.gauss_log_norm(var.astype(np.float32)) + dist)
+        assert abs(sc[0] - sc[1]) <= 1e-4 * max(1.0, abs(sc[1])), (ti, ei, b[ti, ei], ref_b[ei, ti], sc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,buffer_size", [("SIMD-diagonal-maximum", 1), ("SIMD-diagonal-maximum", 7),
+                                              ("SIMD-diagonal-maximum", 64), ("diagonal-maximum", 1),
+                                              ("diagonal-maximum", 64), ("diagonal-sum", 64)])
+def test_aligner_sparse_best_densities(gpu, tmp_path, kind, buffer_size):
+    """An aligner's read (AbstractMixtureSetEstimator.cc:370-384): score(e) of every emission and
+    bestDensity(e) of 1-10 emissions per frame.  The positions of calls made before the first bestDensity() answer
+    it one pair at a time (gmm_best_density_pairs, up to kSparseMax pairs per call, then the call's whole table);
+    every later call carries the best densities (prefetches included).  SIMD bit-exact against the restatement,
+    the float types within the near-tie rule; the frames the consumer never asked stay 0xffffffff."""
+    counts = ra.ragged_counts(30, 30 * 9, low=1, high=90, seed=67)  # mixtures of 1 .. 90 densities (two waves' scan)
+    ms = ra.synthetic_mixture_set(30, counts, 39, seed=67, weights="random")
+    frames = ra.synthetic_frames(300, 39, seed=68)
+    s, b, _ = _run(tmp_path, ms, frames, kind, buffer_size, 2, protocol="aligner")
+    asked = b != 0xFFFFFFFF
+    assert asked.sum() >= 300 and asked.sum(axis=1).max() <= 10
+    if kind == "SIMD-diagonal-maximum":
+        ref_s, ref_b, _ = oracle.OracleSimd(ms).score(frames)
+        assert np.array_equal(s.T.view(np.uint32), ref_s.view(np.uint32))
+        assert np.array_equal(b[asked], ref_b.T[asked])
+    else:
+        of = oracle.OracleFloatSum(ms) if kind == "diagonal-sum" else oracle.OracleFloat(ms)
+        ref_s, ref_b = of.score(frames)[:2]
+        assert (np.abs(s.T.astype(np.float64) - ref_s) / np.maximum(1, np.abs(ref_s))).max() <= 1e-4
+        _near_tie_ok(ms, frames.astype(np.float64), b, ref_b, asked)
