@@ -273,12 +273,21 @@ struct gmm_scorer {
 
 namespace {
 
+// the split scorer runs scoreSplitWide (gmm_kernels_split.hip launchSplitK: 16-row tiles, no preselection, not
+// diagonal-sum, K steps with a wide instantiation)
+bool splitWideOf(const gmm_scorer* s) {
+    return s->split && s->splitRows == 16 && !s->presel && s->flavor != Flavor::DiagonalSum &&
+           splitWideFrames(s->kSteps16) != 0;
+}
+
 uint32_t framesPerBlock(const gmm_scorer* s) {
     if (s->quantized)
         return s->presel ? kI8PreselFramesPerBlock : kI8FramesPerBlock;
     if (s->direct)
         return kDirectFramesPerBlock;
-    return s->split ? kSplitFramesPerBlock : kF32FramesPerBlock;
+    if (!s->split)
+        return kF32FramesPerBlock;
+    return splitWideOf(s) ? splitWideFrames(s->kSteps16) : kSplitFramesPerBlock;
 }
 
 // the frame tile of one call: the quantized kernels take 256-frame tiles for calls of up to 256 frames and
@@ -343,6 +352,11 @@ int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
             : s->quantized && !s->presel ? std::clamp<uint32_t>(nFrameTiles * 1024u, 2048u, uint32_t(GMM_TARGET_BLOCKS))
                                          : uint32_t(GMM_TARGET_BLOCKS);
     uint32_t       target        = std::max<uint32_t>(1, (kTargetBlocks + nFrameTiles - 1) / nFrameTiles);
+    // whole rounds of the 8 XCDs: mapBlock gives XCD x the chunks x, x + 8, ..., so a count just past a multiple of 8
+    // leaves most XCDs idle for the last chunk (12 chunks of 171 192-frame tiles: 7.59 ms against 5.51 for 16 chunks
+    // of 128 256-frame tiles at D = 45, profiles/r05/s15)
+    if (target > 8)
+        target = (target + 7u) / 8u * 8u;
     target                       = std::min<uint32_t>(target, std::max<uint32_t>(1, s->nMix));
     const uint32_t T             = s->nTiles;
     const uint32_t perChunk      = std::max<uint32_t>(1, (T + target - 1) / target);
@@ -1416,6 +1430,11 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
         s->split    = p.split;
         s->kSteps16 = p.kSteps16;
         s->splitRows = p.splitRows;
+        // wide workgroups of 192 frames (K steps 5) read up to 191 rows past the call: room for them in the frame
+        // tables, which are laid out in 512-frame quanta
+        if (splitWideOf(s.get()) && kSplitFramesPerBlock % splitWideFrames(s->kSteps16) != 0)
+            s->nFramesPad = (cfg.max_frames + splitWideFrames(s->kSteps16) + kFramePadQuantum - 1) / kFramePadQuantum *
+                            kFramePadQuantum;
         s->nMix       = p.nMixtures;
         s->kSteps     = p.kSteps;
         s->multiCov   = s->C > 1;
@@ -1659,6 +1678,7 @@ int gmm_scorer_create_sharded(const gmm_mixture_set* ms, gmm_scorer_type type, c
     s->split      = m ? m->split : false;
     s->direct     = m ? m->direct : false;
     s->splitRows  = m ? m->splitRows : 16;
+    s->kSteps16   = m ? m->kSteps16 : 0;
     s->device     = g->lead;
     s->cfg        = cfg;
     s->D          = ms->dimension;

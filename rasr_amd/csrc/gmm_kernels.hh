@@ -110,6 +110,13 @@ constexpr uint32_t kSplitFramesPerBlock = GMM_SPLIT_FPB;  // frames per workgrou
 constexpr uint32_t kSplitWaves          = kSplitFramesPerBlock / 64;  // 64 frames per wave: scoreSplit32,
                                                                       // scoreSplitSum, preselection-batch-float
 constexpr uint32_t kSplitMainWaves      = kSplitFramesPerBlock / (16 * kSplitNF);  // scoreSplit
+#ifndef GMM_SPLIT_WIDE
+#define GMM_SPLIT_WIDE 1  // scoreSplitWide for K steps <= 5 without preselection (0: the pair kernel, A/B)
+#endif
+// scoreSplitWide (16-row tiles, diagonal-maximum / batch-float without preselection): frames of its one-wave
+// workgroups at ks K steps -- 16 column blocks at K <= 128, 12 at K = 160 (the frame operands fill <= 256 AGPRs) --
+// or 0 where the pair kernel scoreSplit runs
+constexpr uint32_t splitWideFrames(uint32_t ks) { return !GMM_SPLIT_WIDE ? 0u : ks <= 4 ? 256u : ks == 5 ? 192u : 0u; }
 
 constexpr uint32_t kSplitLimbs   = 4;
 constexpr uint32_t kSplitXXLimbs = 3;

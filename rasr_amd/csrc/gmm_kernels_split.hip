@@ -217,9 +217,13 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
 // scheduled into): uniform options are arithmetic, the frame bound is the buffer's num_records.
 // ---------------------------------------------------------------------------
 template <bool BEST>
+__device__ __forceinline__ void emitKeysSplit(const SplitArgs& a, const uint32_t (&k)[4], uint32_t m, uint32_t frame0,
+                                              int lane, uint32_t g, uint32_t kmask, int eOut, float noneScore);
+
+template <bool BEST>
 __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint32_t (&best)[4][4], uint32_t m,
                                                  uint32_t frame0, int lane, uint32_t g, uint32_t kmask, int eOut,
-                                                 float noneScore, float halfScale) {
+                                                 float noneScore) {
 #if GMM_SPLIT_DIAG_NOEMIT  // diagnostic (wrong results): the emit's cost, the minima kept live by one XOR chain
     {
         uint32_t x = 0;
@@ -242,6 +246,14 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
         else
             k[cb] = min(umin3(best[cb][0], best[cb][1], best[cb][2]), best[cb][3]);
     }
+    emitKeysSplit<BEST>(a, k, m, frame0, lane, g, kmask, eOut, noneScore);
+}
+
+// the per-block minima k[cb] (over the block's slots, lane group g of the tile rows in every lane) -> (score,
+// density) of frame frame0 + lane
+template <bool BEST>
+__device__ __forceinline__ void emitKeysSplit(const SplitArgs& a, const uint32_t (&k)[4], uint32_t m, uint32_t frame0,
+                                              int lane, uint32_t g, uint32_t kmask, int eOut, float noneScore) {
     // groups {g&1, g&1|2} of blocks (0,2) and (1,3): lanes < 32 keep blocks 0, 1, lanes >= 32 blocks 2, 3
     uint32_t w[2], wg[2];
 #pragma unroll
@@ -268,7 +280,6 @@ __device__ __forceinline__ void emitMixtureSplit(const SplitArgs& a, const uint3
     const float score = none ? noneScore
                              : __fmul_rn(a.outScale, (a.flavor == 3 && !(total < 3.40282347e+38f)) ? total : 0.5f * total);
     const uint32_t idx = none ? 0xffffffffu : ((((key & kmask) >> 2) << 4) | (grp << 2) | (key & 3u));
-    (void)halfScale;
     const uint32_t mo  = m - a.mixBase;
     const uint32_t off = static_cast<uint32_t>(frame0 + lane) * 4u;
     // frames >= nFrames fall outside num_records: the buffer store drops them
@@ -467,7 +478,7 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
 #pragma unroll
         for (int h = 0; h < NH; ++h)
             emitMixtureSplit<BEST>(a, *reinterpret_cast<const uint32_t(*)[4][4]>(&best[4 * h]), m, frame0 + 64u * h,
-                                   lane, g, kmask, eOut[h], noneScore, 0.5f);
+                                   lane, g, kmask, eOut[h], noneScore);
     };
     // after an emit at tile tNext: next mixture, and the empty ones that also end there (rare path)
     const auto advance = [&](uint32_t tNext) __attribute__((always_inline)) {
@@ -554,6 +565,186 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
                 }
                 else {
                     drain(acc[i % 2], tt - 2, TT[i % 2]);
+                    live = false;
+                }
+            }
+        });
+    }
+}
+
+// ---------------------------------------------------------------------------
+// scoreSplitWide (GMM_SPLIT_WIDE; no preselection): one wave per workgroup holds NF column blocks of 16 frames --
+// 16 (256 frames) at K steps <= 4 (D <= 40), 12 (192 frames) at 5 (D <= 51), whose f16 fragments fill the
+// accumulator file (256 / 240 AGPRs) -- and walks its chunk ONE tile per pipeline step: the tile's NF x KS MFMAs
+// beside the epilogue of the previous tile.  Against scoreSplit's 128-frame waves every tile fragment a wave loads
+// feeds 2x (1.5x) the MFMAs (less L2-to-CU traffic and per-tile address and loop work per MFMA), and the frame tiles
+// of a chunk run at once on one XCD (4 one-wave workgroups per CU), so the chunk streams through its L2 about once.
+// The min3 takes two slots of the same tile (rows 4g + r: the key's tag carries r), two running minima per block.
+// ---------------------------------------------------------------------------
+#ifndef GMM_SPLIT_WIDE_PF
+#define GMM_SPLIT_WIDE_PF 3  // tiles in flight
+#endif
+#ifndef GMM_SPLIT_WIDE_IL
+#define GMM_SPLIT_WIDE_IL 48  // MFMAs of a step interleaved 1 : 2 with the epilogue's VALU (at 16 blocks)
+#endif
+
+template <int KS, bool BEST>
+__global__ __launch_bounds__(64, 1) void scoreSplitWide(SplitArgs a, const uint32_t* __restrict__ mixTileOff) {
+    constexpr uint32_t FPB = splitWideFrames(KS);  // frames of the workgroup's one wave
+    constexpr int      NF = FPB / 16, NH = NF / 4, PF = GMM_SPLIT_WIDE_PF, U = PF % 2 == 0 ? PF : 2 * PF;
+    static_assert(FPB != 0 && NF * KS * 4 <= 256, "the frame operands fill at most the accumulator file");
+    const int      lane = threadIdx.x & 63;
+    const uint32_t g    = static_cast<uint32_t>(lane) >> 4;
+    uint32_t       chunk, ft;
+    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
+        return;
+    const uint32_t frame0 = ft * FPB, fb0 = frame0 / 16u;
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
+
+    const f16x8* th       = static_cast<const f16x8*>(a.tileH);
+    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS]) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+    };
+    const f16x8* fh = static_cast<const f16x8*>(a.frameH);
+    f16x8        B[NF][KS];
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            B[cb][s] = fh[(static_cast<size_t>(fb0 + cb) * KS + s) * 64 + lane];
+    int eOut[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+        eOut[h] = a.frameExp[frame0 + 64u * h + lane];
+    // the frame operands complete before the tile prefetch, then pinned to the accumulator file
+#pragma unroll
+    for (int cb = 0; cb < NF; ++cb)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            asm volatile("" : "+a"(B[cb][s]));
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+        asm volatile("" ::"v"(eOut[h]));
+
+    f16x8 R[PF][KS];  // tile j (from T0) in set j % PF; the tile array's kTilePad tiles keep prefetches in bounds
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+        loadTile(T0 + j, R[j]);
+
+    const uint32_t kmask = BEST ? (1u << a.tileBits) - 1u : 0u;
+    uint32_t       vmask = ~kmask;
+    asm volatile("" : "+v"(vmask));
+    const float noneScore = __fmul_rn(a.outScale, a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f);
+
+    uint32_t   best[NF][2];  // slot 0: rows 4g, 4g + 1; slot 1: rows 4g + 2, 4g + 3
+    const auto resetBest = [&]() {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+            best[cb][0] = best[cb][1] = 0xffffffffu;
+    };
+    const auto chain = [&](const f16x8(&A)[KS], f32x4(&acc)[NF]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+            acc[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int cb = 0; cb < NF; ++cb)
+                acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[s], B[cb][s], acc[cb], 0, 0, 0);
+    };
+    const auto epilogue = [&](const f32x4(&acc)[NF], uint32_t tl) __attribute__((always_inline)) {
+        uint32_t tag[4];  // opaque SGPRs: one v_and_or_b32 per value
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            tag[r] = (tl << 2) | static_cast<uint32_t>(r);
+            asm("" : "+s"(tag[r]));
+        }
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb) {
+            uint32_t v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                v[r] = BEST ? (__float_as_uint(acc[cb][r]) & vmask) | tag[r] : __float_as_uint(acc[cb][r]);
+            best[cb][0] = umin3(best[cb][0], v[0], v[1]);
+            best[cb][1] = umin3(best[cb][1], v[2], v[3]);
+        }
+    };
+
+    uint32_t   m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
+    const auto emit = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            uint32_t k[4];
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+                k[cb] = min(best[4 * h + cb][0], best[4 * h + cb][1]);
+            emitKeysSplit<BEST>(a, k, m, frame0 + 64u * h, lane, g, kmask, eOut[h], noneScore);
+        }
+    };
+    const auto advance = [&](uint32_t tNext) __attribute__((always_inline)) {
+        ++m;
+        tBeg = tNext;
+        tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        while (m < m1 && tEnd == tNext) {
+            emit();
+            ++m;
+            tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        }
+    };
+    const auto finish = [&](uint32_t tNext) __attribute__((always_inline)) {
+        if (tNext == tEnd) {
+            emit();
+            resetBest();
+            advance(tNext);
+        }
+    };
+    constexpr int kIl = GMM_SPLIT_WIDE_IL * NF / 16;  // MFMAs with 2 VALU each: the 6 NF epilogue VALU
+    const auto    step = [&](const f16x8(&A)[KS], f32x4(&cur)[NF], const f32x4(&prev)[NF], uint32_t tPrev)
+            __attribute__((always_inline)) {
+        chain(A, cur);
+        epilogue(prev, tPrev - tBeg);
+#pragma unroll
+        for (int i = 0; i < kIl; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NF * KS - kIl, 0);
+    };
+
+    resetBest();
+    while (m < m1 && tEnd == T0) {  // mixtures without tiles at the start of the chunk
+        emit();
+        ++m;
+        tEnd = m < m1 ? mixTileOff[m + 1] : T0;
+    }
+    if (T0 < T1) {
+        f32x4 acc[2][NF];
+        chain(R[0], acc[0]);  // tile T0: nothing to finish beside it
+        loadTile(T0 + PF, R[0]);
+        uint32_t t = T0 + 1;
+        // tile tt = T0 + j with j = 1 + i (mod U): operands R[j % PF], accumulators acc[j % 2]
+        const auto sub = [&](auto ic, uint32_t tt) __attribute__((always_inline)) {
+            constexpr int i = decltype(ic)::value, set = (1 + i) % PF, cur = (1 + i) % 2, prv = i % 2;
+            step(R[set], acc[cur], acc[prv], tt - 1);
+            loadTile(tt + PF, R[set]);
+            finish(tt);
+        };
+        for (; t + U <= T1; t += U)
+            staticFor<U>([&](auto ic) __attribute__((always_inline)) { sub(ic, t + decltype(ic)::value); });
+        bool live = true;
+        staticFor<U>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int  i  = decltype(ic)::value;
+            const uint32_t tt = t + i;
+            if (live) {
+                if (tt < T1) {
+                    sub(ic, tt);
+                }
+                else {  // the last tile's epilogue
+                    epilogue(acc[i % 2], tt - 1 - tBeg);
+                    finish(tt);
                     live = false;
                 }
             }
@@ -1096,6 +1287,15 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
 
 template <int KS>
 static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
+    if constexpr (splitWideFrames(KS) != 0) {
+        if (!a.presel) {
+            if (a.best)
+                hipLaunchKernelGGL((dev::scoreSplitWide<KS, true>), dim3(grid), dim3(64), 0, s, a, a.mixTileOff);
+            else
+                hipLaunchKernelGGL((dev::scoreSplitWide<KS, false>), dim3(grid), dim3(64), 0, s, a, a.mixTileOff);
+            return;
+        }
+    }
     if (a.presel) {  // preselection-batch-float: no best density; the waves' mask tables in dynamic LDS
         // the block's 256 frames = 4 tables of [clusters][16] words, whatever the waves
         const uint32_t lds = kSplitFramesPerBlock / 64u * a.nClusters * 64u;
