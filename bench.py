@@ -308,7 +308,7 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         d_local = int(ms.n_entries)
     algo = 2.0 * args.dim * d_local * fpl  # one multiply-add per (frame, density, component), per launch
     kernel = sc.main_kernel()
-    split = kernel in ("scoreSplit", "scoreSplit32", "scoreSplitSum")
+    split = kernel in ("scoreSplit", "scoreSplitWide", "scoreSplit32", "scoreSplitSum")
     if split:
         # f32-accurate contraction on the f16 matrix cores: 3 f16 products per f32 multiply-add, so the
         # roofline for this arithmetic is the dense f16 peak / 3; the MFMA work actually issued covers

@@ -282,7 +282,8 @@ bool splitWideOf(const gmm_scorer* s) {
 
 uint32_t framesPerBlock(const gmm_scorer* s) {
     if (s->quantized)
-        return s->presel ? kI8PreselFramesPerBlock : kI8FramesPerBlock;
+        return s->presel ? kI8PreselFramesPerBlock
+                         : (s->scoreOnly == kScoreOnlySlots ? kI8ClsFramesPerBlock : kI8FramesPerBlock);
     if (s->direct)
         return kDirectFramesPerBlock;
     if (!s->split)
@@ -1359,6 +1360,9 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
         s->scoreOnly = p.scoreOnly;
+        // scoreI8Cls workgroups of kI8ClsFramesPerBlock frames: the frame tables hold whole workgroups
+        if (s->scoreOnly == kScoreOnlySlots && !presel && kI8ClsFramesPerBlock > kFramePadQuantum)
+            s->nFramesPad = (cfg.max_frames + kI8ClsFramesPerBlock - 1) / kI8ClsFramesPerBlock * kI8ClsFramesPerBlock;
         if (p.scoreOnly && (rc = upload(&s->dMixOddMask, p.mixOddMask)) != GMM_OK)
             return rc;
         s->nMix            = p.nMixtures;
@@ -1986,7 +1990,7 @@ int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLau
         *nLaunches = s->presel ? 3 : 2;
     if (name)
         *name = s->quantized ? "scoreI8" : s->direct ? "scoreDirect" : (s->split ? (s->flavor == Flavor::DiagonalSum ? "scoreSplitSum"
-                                                                         : (s->splitRows == 32 ? "scoreSplit32" : "scoreSplit"))
+                                                                         : (s->splitRows == 32 ? "scoreSplit32" : (splitWideOf(s) ? "scoreSplitWide" : "scoreSplit")))
                                                        : "scoreF32");
     return GMM_OK;
 }

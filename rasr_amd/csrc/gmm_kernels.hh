@@ -38,6 +38,11 @@ constexpr int      kI8NF          = GMM_I8_NF;   // column blocks of 16 frames p
 constexpr int      kF32NF         = GMM_F32_NF;  // column blocks of 16 frames per wave, float kernel
 constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kI8FramesPerBlock  = kWavesPerBlock * kI8NF * 16;   // 512
+#ifndef GMM_I8_CLS_NF
+#define GMM_I8_CLS_NF 16  // scoreI8Cls (calls without best densities, slot layout): column blocks per wave (8 or 16)
+#endif
+constexpr int      kI8ClsNF           = GMM_I8_CLS_NF;
+constexpr uint32_t kI8ClsFramesPerBlock = kWavesPerBlock * kI8ClsNF * 16;
 constexpr uint32_t kI8SmallFrames     = kWavesPerBlock * 4 * 16;        // 256: the small-call tile (I8Args::smallTile)
 constexpr uint32_t kI8TinyFrames      = 4 * 16;                         // 64: one 64-frame wave per workgroup
 constexpr uint32_t kF32FramesPerBlock = kWavesPerBlock * kF32NF * 16;  // 256
@@ -111,12 +116,17 @@ constexpr uint32_t kSplitWaves          = kSplitFramesPerBlock / 64;  // 64 fram
                                                                       // scoreSplitSum, preselection-batch-float
 constexpr uint32_t kSplitMainWaves      = kSplitFramesPerBlock / (16 * kSplitNF);  // scoreSplit
 #ifndef GMM_SPLIT_WIDE
-#define GMM_SPLIT_WIDE 1  // scoreSplitWide for K steps <= 5 without preselection (0: the pair kernel, A/B)
+#define GMM_SPLIT_WIDE 1  // scoreSplitWide for K steps <= 4 without preselection (0: the pair kernel, A/B)
+#endif
+#ifndef GMM_SPLIT_WIDE5
+#define GMM_SPLIT_WIDE5 0  // 192-frame waves at K steps 5 (A/B: no faster than the pair kernel)
 #endif
 // scoreSplitWide (16-row tiles, diagonal-maximum / batch-float without preselection): frames of its one-wave
-// workgroups at ks K steps -- 16 column blocks at K <= 128, 12 at K = 160 (the frame operands fill <= 256 AGPRs) --
-// or 0 where the pair kernel scoreSplit runs
-constexpr uint32_t splitWideFrames(uint32_t ks) { return !GMM_SPLIT_WIDE ? 0u : ks <= 4 ? 256u : ks == 5 ? 192u : 0u; }
+// workgroups at ks K steps -- 16 column blocks at K <= 128 (the frame operands fill the 256 AGPRs) -- or 0 where the
+// pair kernel scoreSplit runs
+constexpr uint32_t splitWideFrames(uint32_t ks) {
+    return !GMM_SPLIT_WIDE ? 0u : ks <= 4 ? 256u : (GMM_SPLIT_WIDE5 && ks == 5) ? 192u : 0u;
+}
 
 constexpr uint32_t kSplitLimbs   = 4;
 constexpr uint32_t kSplitXXLimbs = 3;

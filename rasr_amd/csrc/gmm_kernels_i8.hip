@@ -899,10 +899,10 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
 // column block; the tile's epilogues follow its MFMAs in the same step (no pending tail).  A frame that selected
 // none of a mixture's densities keeps all ones: Core::Type<int>::max, as the reference.
 template <int NF, int SEG, int W, bool PRESEL = false>
-__global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : 4) : 1) void scoreI8Cls(I8Args a, const uint32_t* __restrict__ mixTileOff,
+__global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : (NF == 16 ? 2 : 4)) : 1) void scoreI8Cls(I8Args a, const uint32_t* __restrict__ mixTileOff,
                                                                                    float* __restrict__ scores,
                                                                                    const uint32_t* __restrict__ mixWord) {
-    static_assert(NF == 4 || NF == 8, "NF");
+    static_assert(NF == 4 || NF == 8 || (NF == 16 && !PRESEL), "NF");
     static_assert(!PRESEL || (NF == 8 && W == 4), "preselection: 128-frame waves (two 64-frame mask words)");
     constexpr int      LAG       = PRESEL ? 0 : GMM_I8_CLS_LAG;
     constexpr int      NPL       = NF / 4;
@@ -1342,8 +1342,9 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
         // workgroups take half of that (more of them per CU)
         constexpr int kSeg = (KS == 1 ? dev::kSegTiles : 8) / (W == 1 ? 2 : 1);
         if constexpr (KS == 1) {
-            if (a.scoreOnly == 2) {  // calls without best densities on the slot layout
-                hipLaunchKernelGGL((dev::scoreI8Cls<NF, kSeg, W>), dim3(grid), dim3(64 * W), 0, s, a, a.mixTileOff,
+            if (a.scoreOnly == 2) {  // calls without best densities on the slot layout (kI8ClsNF blocks per wave)
+                constexpr int NFC = (W == 4 && NF == kI8NF) ? kI8ClsNF : NF;
+                hipLaunchKernelGGL((dev::scoreI8Cls<NFC, kSeg, W>), dim3(grid), dim3(64 * W), 0, s, a, a.mixTileOff,
                                    a.scores, a.mixOddMask);
                 return;
             }
