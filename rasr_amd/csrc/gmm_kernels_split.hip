@@ -797,16 +797,22 @@ __device__ __forceinline__ void emitMixtureSplit32(const SplitArgs& a, const uin
     }
 }
 
+#ifndef GMM_SPLIT32_NB
+#define GMM_SPLIT32_NB 4  // 32-frame column blocks per wave of scoreSplit32 (4: 128 frames, B in the AGPRs; 2: 64)
+#endif
+
 template <int KS, bool BEST>
-__global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSplit32(SplitArgs a,
-                                                                        const uint32_t* __restrict__ mixTileOff) {
+__global__ __launch_bounds__(64 * (kSplitFramesPerBlock / (32 * GMM_SPLIT32_NB)), GMM_SPLIT_MIN_WAVES) void scoreSplit32(
+        SplitArgs a, const uint32_t* __restrict__ mixTileOff) {
     typedef float f32x16 __attribute__((ext_vector_type(16)));
+    constexpr int NB = GMM_SPLIT32_NB, NH = NB / 2;  // blocks of 32 frames; halves of 64 frames (one emit each)
+    static_assert(NB == 2 || NB == 4, "64 or 128 frames per wave");
     const int      lane = threadIdx.x & 63;
     const int      wave = threadIdx.x >> 6;
     uint32_t       chunk, ft;
     if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
         return;
-    const uint32_t frame0 = ft * kSplitFramesPerBlock + static_cast<uint32_t>(wave) * 64u;
+    const uint32_t frame0 = ft * kSplitFramesPerBlock + static_cast<uint32_t>(wave) * (32u * NB);
     const uint32_t fb0    = frame0 / 32u;
     const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
     const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
@@ -818,20 +824,28 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
     };
     const f16x8* fh = static_cast<const f16x8*>(a.frameH);
-    f16x8        B[2][KS];
+    f16x8        B[NB][KS];
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int s = 0; s < KS; ++s)
             B[b][s] = fh[(static_cast<size_t>(fb0 + b) * KS + s) * 64 + lane];
-    const int eOut = a.frameExp[frame0 + lane];
-    // frame operands complete before the tile prefetch (see scoreSplit)
+    int eOut[NH];
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int h = 0; h < NH; ++h)
+        eOut[h] = a.frameExp[frame0 + 64u * h + lane];
+    // frame operands complete before the tile prefetch (see scoreSplit); 128-frame waves keep them in the AGPRs
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-            asm volatile("" ::"v"(B[b][s]));
-    asm volatile("" ::"v"(eOut));
+            if constexpr (NB == 4)
+                asm volatile("" : "+a"(B[b][s]));
+            else
+                asm volatile("" ::"v"(B[b][s]));
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+        asm volatile("" ::"v"(eOut[h]));
 
     f16x8 R0[KS], R1[KS];  // tiles t (even steps) and t + 1; padded tile array: loads past T1 stay in bounds
     loadTile(T0, R0);
@@ -842,25 +856,25 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
     asm volatile("" : "+v"(vmask));
     const float noneScore = __fmul_rn(a.outScale, a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f);
 
-    uint32_t   best[2][4];
+    uint32_t   best[NB][4];
     const auto resetBest = [&]() {
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 best[b][q] = 0xffffffffu;
     };
-    const auto chain = [&](const f16x8(&A)[KS], f32x16(&acc)[2]) {
+    const auto chain = [&](const f16x8(&A)[KS], f32x16(&acc)[NB]) {
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < NB; ++b)
             acc[b] = f32x16{};  // ||x'||^2 is in K: the chain starts from an inline 0
 #pragma unroll
         for (int s = 0; s < KS; ++s)
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < NB; ++b)
                 acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[b][s], acc[b], 0, 0, 0);
     };
-    const auto epilogue = [&](const f32x16(&acc)[2], uint32_t tl) {
+    const auto epilogue = [&](const f32x16(&acc)[NB], uint32_t tl) {
         uint32_t tag[16];  // opaque SGPRs (one v_and_or_b32 per value)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -868,7 +882,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
             asm("" : "+s"(tag[i]));
         }
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if constexpr (!BEST) {  // scores only: the values' own bits
@@ -886,7 +900,12 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
 
     uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
     resetBest();
-    const auto emit    = [&]() { emitMixtureSplit32<BEST>(a, best, m, frame0, lane, kmask, eOut, noneScore); };
+    const auto emit = [&]() {
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            emitMixtureSplit32<BEST>(a, *reinterpret_cast<const uint32_t(*)[2][4]>(&best[2 * h]), m, frame0 + 64u * h,
+                                     lane, kmask, eOut[h], noneScore);
+    };
     const auto advance = [&](uint32_t tNext) {
         ++m;
         tBeg = tNext;
@@ -905,11 +924,11 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         }
     };
     // MFMAs of the tile in A into cur beside the epilogue of tile tPrev (in prev), 1 MFMA : 3 VALU
-    const auto step = [&](const f16x8(&A)[KS], f32x16(&cur)[2], const f32x16(&prev)[2], uint32_t tPrev) {
+    const auto step = [&](const f16x8(&A)[KS], f32x16(&cur)[NB], const f32x16(&prev)[NB], uint32_t tPrev) {
         chain(A, cur);
         epilogue(prev, tPrev - tBeg);
 #pragma unroll
-        for (int i = 0; i < 2 * KS; ++i) {
+        for (int i = 0; i < NB * KS; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
         }
@@ -921,7 +940,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, GMM_SPLIT_MIN_WAVES) void scoreSp
         tEnd = m < m1 ? mixTileOff[m + 1] : T0;
     }
     if (T0 < T1) {
-        f32x16   accX[2], accY[2];
+        f32x16   accX[NB], accY[NB];
         uint32_t t = T0;
         chain(R0, accX);  // tile T0: nothing to finish beside it
         loadTile(t + 2, R0);
@@ -1315,9 +1334,11 @@ static void launchSplitK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
 template <int KS>
 static void launchSplit32K(const SplitArgs& a, uint32_t grid, hipStream_t s) {
     if (a.best)
-        hipLaunchKernelGGL((dev::scoreSplit32<KS, true>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit32<KS, true>), dim3(grid), dim3(64 * (kSplitFramesPerBlock / (32 * GMM_SPLIT32_NB))),
+                           0, s, a, a.mixTileOff);
     else
-        hipLaunchKernelGGL((dev::scoreSplit32<KS, false>), dim3(grid), dim3(64 * kSplitWaves), 0, s, a, a.mixTileOff);
+        hipLaunchKernelGGL((dev::scoreSplit32<KS, false>), dim3(grid), dim3(64 * (kSplitFramesPerBlock / (32 * GMM_SPLIT32_NB))),
+                           0, s, a, a.mixTileOff);
 }
 
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps16, hipStream_t stream) {

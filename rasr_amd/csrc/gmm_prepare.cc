@@ -670,10 +670,11 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
     const uint32_t keyBits16 = bitsFor(((maxEntries + 15) / 16 + 1) & ~1u) + 2;
     const bool     fits32    = keyBits32 <= 8 && splitKSteps32(D) <= kSplit32MaxKSteps;
     // 32-row tiles only where they save more K than the clock they cost: the 32x32x16 loop holds a lower clock
-    // than the 16x16x32 one on this power-bound kernel (MI355X_MICROARCH.md DVFS item 7), measured at D = 45
-    // (K 144 vs 160) as 5.90 vs 5.70 ms per 32768 frames, i.e. ~1.15x the time per K column
-    // (profiles/r02/ab/ab_d45_shape.txt)
-    const bool     saves32   = splitKSteps32(D) * 16 * 115 < splitKSteps(D) * 32 * 100;
+    // than the 16x16x32 one on this power-bound kernel (MI355X_MICROARCH.md DVFS item 7).  With 64-frame waves that
+    // was ~1.15x the time per K column (D = 45: 5.90 vs 5.70 ms, profiles/r02/ab/ab_d45_shape.txt); with 128-frame
+    // waves (round 5) the 32-row kernel is the faster one at D = 45 (5.308 vs 5.368 ms, K 144 vs 160, ~1.05x per
+    // K column, profiles/r05/s20)
+    const bool     saves32   = splitKSteps32(D) * 16 * 105 < splitKSteps(D) * 32 * 100;
     const bool     want32    = splitRowsWanted == 32 || (splitRowsWanted == 0 && saves32);
     // diagonal-sum: 16-row tiles only (scoreSplitSum)
     const uint32_t rows      = (flavor != Flavor::DiagonalSum && fits32 && (want32 || keyBits16 > 8))
