@@ -230,11 +230,14 @@ def _kernel_id() -> str:
     return _capi.load_library().gmm_kernel_id().decode()
 
 
-def load_pmc(mode: str, frames_per_launch: int):
+def load_pmc(mode: str, frames_per_launch: int, default_model: bool = True):
     """HBM bytes per launch of the dominant kernel from the rocprofv3 PMC summary under profiles/
     (scripts/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE), used only when it
-    was collected on this build's kernels (gmm_kernel_id) at this launch size; else null."""
+    was collected on this build's kernels (gmm_kernel_id) at this launch size and on the model the summaries are
+    profiled on (scripts/profile_pmc.sh: the default 39-dim, 160-density bench model); else null."""
     path = os.path.join(ROOT, "profiles", f"pmc_{mode}.json")
+    if not default_model:
+        return None, f"{os.path.relpath(path, ROOT)} is profiled on the default model, not this one"
     try:
         with open(path) as f:
             pmc = json.load(f)
@@ -326,7 +329,8 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         issued = 2.0 * 64 * ((args.dim + 63) // 64) * d_local * fpl
     sec = kms_avg * 1e-3
     achieved = algo / sec / 1e12
-    traffic, traffic_src = load_pmc(mode, fpl) if not sharded else (None, None)
+    default_model = args.dim == 39 and not args.ragged and args.mixtures == 5000 and args.densities == 160
+    traffic, traffic_src = load_pmc(mode, fpl, default_model) if not sharded else (None, None)
     res = {
         "value": total_frames / dt_max,
         "ms_per_step": dt_max / args.steps * 1e3,
