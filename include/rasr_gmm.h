@@ -75,11 +75,16 @@ typedef struct {
     uint32_t mixture_end;
     uint32_t flags;                /* GMM_FLAG_* bits, 0 = defaults                                               */
     /* density preselection (preselection-batch-*): the "density-clustering" parameters,
-     * DensityClustering.cc:19-32.  The clustering is built at create time (no cache-archive). */
+     * DensityClustering.cc:19-32.  The clustering is built (or read from cache_archive) at create time. */
     uint32_t clusters;              /* "clusters" (256, range 1..256), reduced to the density count      */
     uint32_t select_clusters;       /* "select-clusters" (32)                                           */
     uint32_t clustering_iterations; /* "iterations" (5)                                                 */
     float    backoff_score;         /* "backoff-score" (40000): float type, mixture with no selected density */
+    /* "cache-archive" (DensityClustering.cc:27-28, 59-95; DensityClustering.tcc:122-155): path of a RASR cache archive
+     * file (Core::MappedArchive).  The preselection types read the clustering from its item "density-clustering" when
+     * magic, version, types, padded dimension, cluster and density counts match, else build it and write the item
+     * there (other items of the archive are kept).  NULL or "": no cache (always built). */
+    const char* cache_archive;
 } gmm_scorer_config;
 
 /* Float types (diagonal-maximum, batch-float) with one covariance run on the f16
@@ -87,8 +92,8 @@ typedef struct {
  * class); this flag selects the f32-MFMA kernel instead. */
 #define GMM_FLAG_NATIVE_F32 1u
 /* Tile height of the split-f16 kernel.  By default 32-density tiles (v_mfma_f32_32x32x16_f16, K in
- * steps of 16) are used where they save more than 15 % of K over 16-density tiles (v_mfma_f32_16x16x32_f16,
- * K in steps of 32; the 32x32 loop holds a lower clock) -- e.g. dimension 9, not 39 or 45 -- and the mixtures
+ * steps of 16) are used where they save more than 5 % of K over 16-density tiles (v_mfma_f32_16x16x32_f16,
+ * K in steps of 32; the 32x32 loop holds a lower clock) -- e.g. dimension 9 or 45, not 39 -- and the mixtures
  * have <= 512 densities, or where a mixture is too large for 16-density tiles; these flags force one
  * height (tests, A/B timing; TILE32 applies only within those limits). */
 #define GMM_FLAG_SPLIT_TILE16 2u
@@ -109,6 +114,9 @@ typedef struct {
  * twin is best effort: if it cannot be built the scorer serves every call from the key layout.  This flag skips
  * it (callers that always ask for best densities, e.g. aligners). */
 #define GMM_FLAG_NO_SCORE_ONLY_TWIN 32u
+/* cache_archive is read-only ("read-only" of the archive, Core/Application.cc:43, 399-400): a clustering that is not
+ * found there is built but not written. */
+#define GMM_FLAG_CACHE_ARCHIVE_READ_ONLY 64u
 
 typedef struct gmm_scorer gmm_scorer;
 
@@ -259,6 +267,14 @@ int gmm_scorer_launch_info(const gmm_scorer* scorer, uint32_t n_frames, uint32_t
  * the summed kernel time and launch count since the last reset. */
 int gmm_scorer_set_timing(gmm_scorer* scorer, int enable);
 int gmm_scorer_kernel_time(gmm_scorer* scorer, double* total_ms, uint32_t* n_launches, int reset);
+
+/* RASR cache archives (Core::MappedArchive, src/Core/MappedArchive.{hh,cc}; the file behind a "cache-archive"
+ * parameter): read item `name` of the archive at `path` -- *size receives its byte count; up to `capacity` bytes are
+ * copied into `data` (may be NULL to ask the size) -- or write it (the archive is created, or rewritten with its other
+ * items kept).  GMM_ERR_INVALID_ARGUMENT if the file is not an archive of that format or has no such item.  Host
+ * only; the preselection scorers use them for the item "density-clustering" (gmm_scorer_config.cache_archive). */
+int gmm_cache_archive_read_item(const char* path, const char* name, void* data, uint64_t capacity, uint64_t* size);
+int gmm_cache_archive_write_item(const char* path, const char* name, const void* data, uint64_t size);
 
 /* Density preselection (preselection-batch-float / -int).
  * gmm_scorer_density_clustering: the clustering the handle was built with, over ALL mixture entries of

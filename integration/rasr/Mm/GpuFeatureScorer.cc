@@ -1,6 +1,7 @@
 // GpuFeatureScorer.cc -- see GpuFeatureScorer.hh.
 #include "GpuFeatureScorer.hh"
 
+#include <Core/Application.hh>
 #include <Mm/FeatureScorerFactory.hh>
 #include <Mm/MixtureSetLoader.hh>
 #include <Mm/Module.hh>
@@ -34,6 +35,8 @@ const Core::ParameterInt GpuFeatureScorer::paramClusteringIterations(
         "iterations", "density clustering iterations", 5, 0);
 const Core::ParameterFloat GpuFeatureScorer::paramBackoffScore(
         "backoff-score", "score of a mixture without a selected density", 40000.0);
+const Core::ParameterString GpuFeatureScorer::paramCacheArchive(
+        "cache-archive", "cache-archive where to cache the clustering of the density preselection", "global-cache");
 
 namespace {
 
@@ -146,6 +149,15 @@ GpuFeatureScorer::GpuFeatureScorer(const Core::Configuration& c, Core::Ref<const
     cfg.selectClusters       = paramSelectClusters(dc);
     cfg.clusteringIterations = paramClusteringIterations(dc);
     cfg.backoffScore         = paramBackoffScore(dc);
+    // the named archive's file and read-only flag, as Core::Application::getCacheArchive resolves them
+    // (Application.cc:397-400); the library opens the file itself (gmm_scorer_config.cache_archive)
+    {
+        static const Core::ParameterString paramFile("file", "cache archive file");  // Application.cc:42-43
+        static const Core::ParameterBool   paramReadOnly("read-only", "whether the cache archive is read-only", false);
+        const Core::Configuration          ac(Core::Application::us()->getConfiguration(), paramCacheArchive(dc));
+        cfg.cacheArchive         = paramFile(ac);
+        cfg.cacheArchiveReadOnly = paramReadOnly(ac);
+    }
     // the batched scorers take the whole buffer into one launch; buffer-size 1 keeps the unbuffered protocol
     // of SIMD-diagonal-maximum / diagonal-maximum (Gpu::createFeatureScorer)
     const Gpu::MixtureSet ms = convertMixtureSet(*mixtureSet);

@@ -45,6 +45,7 @@ public:
     static const Core::ParameterInt   paramSelectClusters;
     static const Core::ParameterInt   paramClusteringIterations;
     static const Core::ParameterFloat paramBackoffScore;
+    static const Core::ParameterString paramCacheArchive;
 
     // scorerType: a reference registration name ("SIMD-diagonal-maximum", "diagonal-maximum",
     // "batch-diagonal-maximum-int", ..., Mm::Gpu::createFeatureScorer)

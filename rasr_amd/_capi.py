@@ -20,6 +20,7 @@ GMM_FLAG_SPLIT_TILE32 = 4
 GMM_FLAG_REFERENCE_ORDER = 8  # diagonal-maximum / batch-float in the reference's f32 operation order
 GMM_FLAG_FULL_KEYS = 16  # batch-int / -fast: (score, density) keys instead of the score-only class layout
 GMM_FLAG_NO_SCORE_ONLY_TWIN = 32  # SIMD: no score-only copy of the model (callers that always want best densities)
+GMM_FLAG_CACHE_ARCHIVE_READ_ONLY = 64  # preselection: read the cached clustering, never write it
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0
@@ -77,6 +78,7 @@ class ScorerConfig(ctypes.Structure):
         ("select_clusters", ctypes.c_uint32),
         ("clustering_iterations", ctypes.c_uint32),
         ("backoff_score", ctypes.c_float),
+        ("cache_archive", ctypes.c_char_p),
     ]
 
 
@@ -139,6 +141,9 @@ PROTOTYPES = [
     ("gmm_scorer_density_clustering", ctypes.c_int,
      [ctypes.c_void_p, _u32p, _u32p, ctypes.c_void_p, ctypes.c_void_p]),
     ("gmm_scorer_cluster_selection", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("gmm_cache_archive_read_item", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    ("gmm_cache_archive_write_item", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64]),
     ("gmm_density_clustering_seeds", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, _u32p]),
     ("gmm_shard_pack_keys", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,

@@ -221,6 +221,7 @@ struct gmm_scorer {
     // density table runs (gmm_score_device with best_density NULL, GMM_HOST_LAZY_BEST host calls): the
     // reference's score(e) without the index-carrying pack, bit-identical scores
     std::unique_ptr<gmm_scorer> scoresOnly;
+    bool clusteringCached = false;  // preselection: the clustering came from the cache archive
     // sparse best densities (gmm_best_density_pairs, gmm_kernels_pairs.hip): entry-major tables of the assigning
     // types in the reference's arithmetic; pairKind -1 where the model has none (e.g. float D > 128)
     int       pairKind = -1;
@@ -627,10 +628,25 @@ namespace {
 int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entryMeans, uint32_t Dp,
                       const std::vector<uint32_t>& rowEntry, const std::vector<uint32_t>* fill) {
     const uint32_t nEntries = ms.mixture_offsets[ms.n_mixtures];
-    std::string    err = buildDensityClustering(s->quantized, entryMeans, nEntries, Dp, s->cfg.clusters,
-                                                s->cfg.select_clusters, s->cfg.clustering_iterations, s->clustering);
-    if (!err.empty())
-        return fail(GMM_ERR_INVALID_ARGUMENT, err);
+    // DensityClustering::build (DensityClustering.tcc:122-155): the cached clustering if the archive holds a matching
+    // one, else build it and cache it
+    const std::string archive = s->cfg.cache_archive ? s->cfg.cache_archive : "";
+    std::vector<char> item;
+    const uint32_t    nClusters = std::min(s->cfg.clusters, nEntries);  // "reducing number of clusters", cc:51-54
+    const bool        cached    = !archive.empty() && nEntries > 0 && s->cfg.select_clusters >= 1 &&
+                         s->cfg.select_clusters <= nClusters && readArchiveItem(archive, "density-clustering", item) &&
+                         decodeClusteringItem(item, s->quantized, Dp, nClusters, nEntries, s->cfg.select_clusters,
+                                              s->clustering);
+    if (!cached) {
+        std::string err = buildDensityClustering(s->quantized, entryMeans, nEntries, Dp, s->cfg.clusters,
+                                                 s->cfg.select_clusters, s->cfg.clustering_iterations, s->clustering);
+        if (!err.empty())
+            return fail(GMM_ERR_INVALID_ARGUMENT, err);
+        // a write failure leaves the scorer as it is (the reference logs it and goes on)
+        if (!archive.empty() && !(s->cfg.flags & GMM_FLAG_CACHE_ARCHIVE_READ_ONLY))
+            (void)writeArchiveItem(archive, "density-clustering", encodeClusteringItem(s->clustering, nEntries));
+    }
+    s->clusteringCached = cached;
     const DensityClustering& dc = s->clustering;
     const uint32_t           T  = static_cast<uint32_t>(rowEntry.size() / kTileRows);
     // per tile row: the byte offset of its cluster in a wave's mask table -- the float kernel's word table
@@ -2076,6 +2092,27 @@ int gmm_scorer_density_clustering(const gmm_scorer* s, uint32_t* nClusters, uint
         else
             std::copy(dc.meansF.begin(), dc.meansF.end(), static_cast<float*>(clusterMeans));
     }
+    return GMM_OK;
+}
+
+int gmm_cache_archive_read_item(const char* path, const char* name, void* data, uint64_t capacity, uint64_t* size) {
+    if (!path || !name || !size)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    std::vector<char> item;
+    if (!readArchiveItem(path, name, item))
+        return fail(GMM_ERR_INVALID_ARGUMENT, std::string("no item ") + name + " in cache archive " + path);
+    *size = item.size();
+    if (data)
+        std::memcpy(data, item.data(), std::min<uint64_t>(capacity, item.size()));
+    return GMM_OK;
+}
+
+int gmm_cache_archive_write_item(const char* path, const char* name, const void* data, uint64_t size) {
+    if (!path || !name || !name[0] || (size && !data))
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument or empty item name");
+    const char* p = static_cast<const char*>(data);
+    if (!writeArchiveItem(path, name, std::vector<char>(p, p + size)))
+        return fail(GMM_ERR_INVALID_ARGUMENT, std::string("cannot write cache archive ") + path);
     return GMM_OK;
 }
 

@@ -2,7 +2,12 @@
 #include "gmm_presel.hh"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
 #include <set>
+
+#include <unistd.h>
 
 #include "gmm_kernels.hh"
 
@@ -148,6 +153,195 @@ std::string buildDensityClustering(bool quantized, const void* entryMeans, uint3
                         out.meansF);
     }
     return "";
+}
+
+// ---------------------------------------------------------------------------
+// cache archive (Core::MappedArchive) and the density-clustering item
+// ---------------------------------------------------------------------------
+namespace {
+constexpr uint32_t kArchiveVersion = 0x17231;  // MappedArchive.cc:52
+
+struct ArchiveItem {
+    std::string       name;
+    std::vector<char> data;
+};
+
+// every item of a valid archive (false: no file, or not an archive of this version; a truncated tail ends the list,
+// as MappedArchive::loadData stops there)
+bool readArchive(const std::string& path, std::vector<ArchiveItem>& items) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in)
+        return false;
+    std::vector<char> all((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    uint32_t          ver = 0;
+    if (all.size() < sizeof(ver))
+        return false;
+    std::memcpy(&ver, all.data(), sizeof(ver));
+    if (ver != kArchiveVersion)
+        return false;
+    size_t o = sizeof(ver);
+    while (o + sizeof(uint32_t) + sizeof(uint64_t) <= all.size()) {
+        uint32_t nl = 0;
+        uint64_t ds = 0;
+        std::memcpy(&nl, all.data() + o, sizeof(nl));
+        std::memcpy(&ds, all.data() + o + sizeof(nl), sizeof(ds));
+        o += sizeof(nl) + sizeof(ds);
+        if (nl == 0 || nl > all.size() - o || ds > all.size() - o - nl)
+            break;
+        ArchiveItem it;
+        it.name.assign(all.data() + o, nl);
+        it.data.assign(all.data() + o + nl, all.data() + o + nl + ds);
+        items.push_back(std::move(it));
+        o += nl + ds;
+    }
+    return true;
+}
+
+struct ItemWriter {
+    std::vector<char> b;
+    template <class T>
+    void pod(const T& v) {
+        const char* p = reinterpret_cast<const char*>(&v);
+        b.insert(b.end(), p, p + sizeof(T));
+    }
+    template <class T>
+    void vec(const T* p, size_t n) {
+        pod<uint64_t>(n);
+        b.insert(b.end(), reinterpret_cast<const char*>(p), reinterpret_cast<const char*>(p) + n * sizeof(T));
+    }
+    void str(const std::string& s) {
+        pod<uint64_t>(s.size() + 1);
+        b.insert(b.end(), s.begin(), s.end());
+        b.push_back(0);
+    }
+};
+
+struct ItemReader {
+    const std::vector<char>& b;
+    size_t                   o  = 0;
+    bool                     ok = true;
+    template <class T>
+    T pod() {
+        T v{};
+        if (!ok || o + sizeof(T) > b.size()) {
+            ok = false;
+            return v;
+        }
+        std::memcpy(&v, b.data() + o, sizeof(T));
+        o += sizeof(T);
+        return v;
+    }
+    template <class T>
+    std::vector<T> vec() {
+        const uint64_t n = pod<uint64_t>();
+        std::vector<T> v;
+        if (!ok || n > (b.size() - o) / sizeof(T)) {
+            ok = false;
+            return v;
+        }
+        v.resize(n);
+        std::memcpy(v.data(), b.data() + o, n * sizeof(T));
+        o += n * sizeof(T);
+        return v;
+    }
+    std::string str() {  // MappedArchiveReader::operator>>(std::string&): up to the first 0
+        const std::vector<char> v = vec<char>();
+        return v.empty() ? std::string() : std::string(v.data(), strnlen(v.data(), v.size()));
+    }
+};
+}  // namespace
+
+bool readArchiveItem(const std::string& path, const std::string& name, std::vector<char>& data) {
+    std::vector<ArchiveItem> items;
+    if (!readArchive(path, items))
+        return false;
+    for (auto it = items.rbegin(); it != items.rend(); ++it)  // MappedArchive::getItem: the last one of a name
+        if (it->name == name) {
+            data = it->data;
+            return true;
+        }
+    return false;
+}
+
+bool writeArchiveItem(const std::string& path, const std::string& name, const std::vector<char>& data) {
+    std::vector<ArchiveItem> items;
+    (void)readArchive(path, items);  // keep the archive's other items (a missing or foreign file starts empty)
+    const std::string tmp = path + ".temp." + std::to_string(static_cast<long>(getpid()));
+    {
+        std::ofstream out(tmp, std::ios::binary | std::ios::trunc);
+        if (!out)
+            return false;
+        out.write(reinterpret_cast<const char*>(&kArchiveVersion), sizeof(kArchiveVersion));
+        const auto put = [&](const std::string& n, const std::vector<char>& d) {
+            const uint32_t nl = static_cast<uint32_t>(n.size());
+            const uint64_t ds = d.size();
+            out.write(reinterpret_cast<const char*>(&nl), sizeof(nl));
+            out.write(reinterpret_cast<const char*>(&ds), sizeof(ds));
+            out.write(n.data(), nl);
+            out.write(d.data(), static_cast<std::streamsize>(ds));
+        };
+        for (const ArchiveItem& it : items)
+            if (it.name != name)
+                put(it.name, it.data);
+        put(name, data);
+        if (!out.good()) {
+            out.close();
+            std::remove(tmp.c_str());
+            return false;
+        }
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) {
+        std::remove(tmp.c_str());
+        return false;
+    }
+    return true;
+}
+
+std::vector<char> encodeClusteringItem(const DensityClustering& dc, uint32_t nEntries) {
+    ItemWriter w;
+    w.str("SPRINT-DC");  // DensityClusteringBase::FileMagic, FileFormatVersion (DensityClustering.cc:34-35)
+    w.pod<uint32_t>(2);
+    w.str(dc.quantized ? "u8" : "f32");  // Core::Type<FeatureType>::name, Core::Type<DistanceType>::name
+    w.str(dc.quantized ? "s32" : "f32");
+    w.pod<uint32_t>(dc.paddedDimension);
+    w.pod<uint32_t>(dc.nClusters);
+    w.pod<uint32_t>(nEntries);
+    w.vec(dc.clusterOfEntry.data(), dc.clusterOfEntry.size());
+    if (dc.quantized)
+        w.vec(dc.meansQ.data(), dc.meansQ.size());
+    else
+        w.vec(dc.meansF.data(), dc.meansF.size());
+    return w.b;
+}
+
+bool decodeClusteringItem(const std::vector<char>& data, bool quantized, uint32_t Dp, uint32_t nClusters,
+                          uint32_t nEntries, uint32_t nSelected, DensityClustering& out) {
+    ItemReader r{data};
+    if (r.str() != "SPRINT-DC" || r.pod<uint32_t>() != 2u)
+        return false;
+    if (r.str() != (quantized ? "u8" : "f32") || r.str() != (quantized ? "s32" : "f32"))
+        return false;
+    if (r.pod<uint32_t>() != Dp || r.pod<uint32_t>() != nClusters || r.pod<uint32_t>() != nEntries || !r.ok)
+        return false;
+    DensityClustering dc;
+    dc.quantized       = quantized;
+    dc.nClusters       = nClusters;
+    dc.nSelected       = nSelected;
+    dc.paddedDimension = Dp;
+    dc.clusterOfEntry  = r.vec<uint8_t>();
+    if (quantized)
+        dc.meansQ = r.vec<uint8_t>();
+    else
+        dc.meansF = r.vec<float>();
+    const size_t nMeans = quantized ? dc.meansQ.size() : dc.meansF.size();
+    // readMeans verifies the size (DensityClustering.tcc:36); every assignment must name a cluster
+    if (!r.ok || dc.clusterOfEntry.size() != nEntries || nMeans != static_cast<size_t>(nClusters) * Dp)
+        return false;
+    for (uint8_t c : dc.clusterOfEntry)
+        if (c >= nClusters)
+            return false;
+    out = std::move(dc);
+    return true;
 }
 
 }  // namespace rasr_gmm

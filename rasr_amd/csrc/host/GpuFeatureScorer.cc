@@ -150,6 +150,9 @@ bool FeatureScorer::init(const MixtureSet& ms, const Configuration& c, uint32_t 
     cfg.select_clusters       = c.selectClusters;
     cfg.clustering_iterations = c.clusteringIterations;
     cfg.backoff_score         = c.backoffScore;
+    cfg.cache_archive         = c.cacheArchive.empty() ? nullptr : c.cacheArchive.c_str();
+    if (c.cacheArchiveReadOnly)
+        cfg.flags |= GMM_FLAG_CACHE_ARCHIVE_READ_ONLY;
     const gmm_mixture_set d  = ms.descriptor();
     const int rc = c.shardDevices.size() > 1
                            ? gmm_scorer_create_sharded(&d, t, &cfg, c.shardDevices.data(),

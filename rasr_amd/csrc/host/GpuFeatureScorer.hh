@@ -130,6 +130,11 @@ struct Configuration {
     uint32_t selectClusters       = 32;
     uint32_t clusteringIterations = 5;
     float    backoffScore         = 40000.0f;
+    // "cache-archive" of "density-clustering" (DensityClustering.cc:27-28), resolved to its file (the archive's
+    // "file" / "read-only", Core/Application.cc:42-43): the clustering is read from / written to its item
+    // "density-clustering"; empty: always built
+    std::string cacheArchive;
+    bool        cacheArchiveReadOnly = false;
 };
 
 // ---------------------------------------------------------------------------

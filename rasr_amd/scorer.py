@@ -6,6 +6,7 @@ Used by the tests and bench.py; RASR itself binds the C-ABI from C++
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -36,7 +37,8 @@ class Scorer:
                  split_tile16: bool = False, split_tile32: bool = False, clusters: int = 256,
                  select_clusters: int = 32, clustering_iterations: int = 5, backoff_score: float = 40000.0,
                  reference_order: bool = False, devices=None, exchange: str = "auto", full_keys: bool = False,
-                 no_score_only_twin: bool = False):
+                 no_score_only_twin: bool = False, cache_archive: str | None = None,
+                 cache_archive_read_only: bool = False):
         self._lib = _capi.load_library()
         self.mixture_set = mixture_set
         self.type = _type_id(scorer_type)
@@ -62,6 +64,11 @@ class Scorer:
         cfg.select_clusters = int(select_clusters)
         cfg.clustering_iterations = int(clustering_iterations)
         cfg.backoff_score = float(backoff_score)
+        # the "density-clustering" item of this RASR cache archive is read if it matches, else built and written
+        self._cache_archive = None if cache_archive is None else os.fsencode(cache_archive)
+        cfg.cache_archive = self._cache_archive
+        if cache_archive_read_only:
+            cfg.flags |= _capi.GMM_FLAG_CACHE_ARCHIVE_READ_ONLY
         if mixture_range is not None:
             cfg.mixture_begin, cfg.mixture_end = int(mixture_range[0]), int(mixture_range[1])
         self.max_frames = int(max_frames)
@@ -267,6 +274,25 @@ class Scorer:
                                                                out.ctypes.data_as(ctypes.c_void_p)),
                     "gmm_scorer_multiply_and_quantize")
         return out
+
+
+def cache_archive_read(path: str, name: str) -> bytes:
+    """Item `name` of a RASR cache archive (Core::MappedArchive layout; gmm_cache_archive_read_item)."""
+    lib = _capi.load_library()
+    size = ctypes.c_uint64()
+    _capi.check(lib.gmm_cache_archive_read_item(os.fsencode(path), name.encode(), None, 0, ctypes.byref(size)),
+                "gmm_cache_archive_read_item")
+    buf = ctypes.create_string_buffer(max(size.value, 1))
+    _capi.check(lib.gmm_cache_archive_read_item(os.fsencode(path), name.encode(), buf, size.value, ctypes.byref(size)),
+                "gmm_cache_archive_read_item")
+    return buf.raw[:size.value]
+
+
+def cache_archive_write(path: str, name: str, data: bytes) -> None:
+    """Write item `name` (the archive is created, or rewritten with its other items kept)."""
+    lib = _capi.load_library()
+    _capi.check(lib.gmm_cache_archive_write_item(os.fsencode(path), name.encode(), data, len(data)),
+                "gmm_cache_archive_write_item")
 
 
 def pinned_empty(shape, dtype=np.float32) -> np.ndarray:

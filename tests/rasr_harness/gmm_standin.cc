@@ -61,6 +61,10 @@ void gmm_default_config(gmm_scorer_config* c) {
 
 const char* gmm_last_error(void) { return gError.c_str(); }
 
+// the cache archive and flags of the last create (the harness checks the adapter's "cache-archive" resolution)
+std::string gStandinCacheArchive;
+uint32_t    gStandinFlags = 0;
+
 int gmm_scorer_create(const gmm_mixture_set* m, gmm_scorer_type type, const gmm_scorer_config* cfg, int device,
                       gmm_scorer** out) {
     (void)device;
@@ -72,6 +76,8 @@ int gmm_scorer_create(const gmm_mixture_set* m, gmm_scorer_type type, const gmm_
     gmm_scorer* s = new gmm_scorer();
     s->type       = type;
     s->cfg        = *cfg;
+    gStandinCacheArchive = cfg->cache_archive ? cfg->cache_archive : "";
+    gStandinFlags        = cfg->flags;
     s->D = m->dimension, s->C = m->n_covariances, s->M = m->n_mixtures;
     const uint32_t nE = m->mixture_offsets[m->n_mixtures];
     s->means.assign(m->means, m->means + static_cast<size_t>(m->n_means) * m->dimension);

@@ -34,6 +34,7 @@
 #include <string>
 #include <vector>
 
+#include <Core/Application.hh>
 #include <Mm/FeatureScorerFactory.hh>
 #include <Mm/ScaledFeatureScorer.hh>
 
@@ -324,6 +325,33 @@ void checkCriticalErrorRouting(const Model& m, const std::vector<float>& frames)
 
 #ifndef HARNESS_PRODUCT
 extern std::vector<int> gStandinShardDevices;  // gmm_standin.cc
+extern "C" std::string  gStandinCacheArchive;  // defined inside gmm_standin.cc's extern "C" block
+extern "C" uint32_t     gStandinFlags;
+
+// "density-clustering.cache-archive" names an archive of the application's configuration; its "file" and
+// "read-only" reach gmm_scorer_config.cache_archive / GMM_FLAG_CACHE_ARCHIVE_READ_ONLY
+// (DensityClustering.cc:27-28, Application.cc:397-400)
+void checkCacheArchiveResolution(const Model& m) {
+    Core::Configuration app = Core::Application::us()->getConfiguration();  // a copy sharing the resources
+    create(m, "SIMD-diagonal-maximum", 1);
+    check(gStandinCacheArchive.empty(), "no global-cache.file -> no cache archive");
+    app.set("global-cache.file", "/tmp/global.cache");
+    create(m, "SIMD-diagonal-maximum", 1);
+    check(gStandinCacheArchive == "/tmp/global.cache" && !(gStandinFlags & GMM_FLAG_CACHE_ARCHIVE_READ_ONLY),
+          "default archive global-cache -> its file");
+    app.set("clustering-cache.file", "/tmp/clustering.cache");
+    app.set("clustering-cache.read-only", "true");
+    Core::Configuration root;
+    root.set("acoustic-model.mixture-set.density-clustering.cache-archive", "clustering-cache");
+    const Core::Configuration c(Core::Configuration(root, "acoustic-model"), "mixture-set");
+    Mm::FeatureScorer* fs = Mm::Module::instance().featureScorerFactory()->createFeatureScorer(
+            idOf("SIMD-diagonal-maximum"), c, Core::Ref<const Mm::AbstractMixtureSet>(m.ms.get()));
+    verify(fs);
+    Core::Ref<Mm::FeatureScorer> keep(fs);
+    check(gStandinCacheArchive == "/tmp/clustering.cache" && (gStandinFlags & GMM_FLAG_CACHE_ARCHIVE_READ_ONLY),
+          "density-clustering.cache-archive -> that archive's file, read-only");
+    std::printf("cache-archive -> gmm_scorer_config.cache_archive \"%s\" read-only\n", gStandinCacheArchive.c_str());
+}
 #endif
 
 int main() {
@@ -376,6 +404,7 @@ int main() {
     }
 #ifndef HARNESS_PRODUCT
     checkCriticalErrorRouting(model, frames);
+    checkCacheArchiveResolution(model);
 #endif
     std::printf("%s (%d failures)\n", gFailures ? "FAILED" : "PASSED", gFailures);
     return gFailures ? 1 : 0;

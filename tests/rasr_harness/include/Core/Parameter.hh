@@ -33,6 +33,35 @@ private:
 };
 typedef Parameter<s32> ParameterInt;
 typedef Parameter<f64> ParameterFloat;
+// Core::ParameterString / ParameterBool: the resource text; "true"/"yes"/"1" for a bool
+class ParameterString {
+public:
+    ParameterString(const char* name, const char* description, const std::string def = "")
+            : name_(name), def_(def) { (void)description; }
+    std::string operator()(const Configuration& c) const {
+        std::string v;
+        return c.get(name_, v) ? v : def_;
+    }
+
+private:
+    std::string name_, def_;
+};
+class ParameterBool {
+public:
+    ParameterBool(const char* name, const char* description, bool def = false) : name_(name), def_(def) {
+        (void)description;
+    }
+    bool operator()(const Configuration& c) const {
+        std::string v;
+        if (!c.get(name_, v))
+            return def_;
+        return v == "true" || v == "yes" || v == "1";
+    }
+
+private:
+    std::string name_;
+    bool        def_;
+};
 // Core::ParameterIntVector (Core/Parameter.hh): values split at `delimiter`, each in [min, max]
 class ParameterIntVector {
 public:
