@@ -5,6 +5,7 @@ Each variant runs in its own subprocess (RASR_GMM_LIB=<so>); rounds are interlea
 (v1 v2 ... v1 v2 ...) and the median / min kernel time per variant is reported.
 usage: ab_bench.py --mode fp32|simd|sum|bint|simds|fp32s|pint|pfloat --rounds 3 lib1.so lib2.so[:split16|:split32|:fullkeys] ...
 (":split16" / ":split32" run that library with GMM_FLAG_SPLIT_TILE16 / _TILE32, ":fullkeys" with GMM_FLAG_FULL_KEYS;
+"@N" at the end sets RASR_GMM_TARGET_BLOCKS=N for that arm, e.g. lib.so@4096 or lib.so:fullkeys@4096;
 bint = batch-diagonal-maximum-int, scores only; simds = SIMD-diagonal-maximum without best densities; fp32s =
 diagonal-maximum without best densities; pint / pfloat = preselection-batch-int / -float)
 """
@@ -59,9 +60,12 @@ def main():
     sums = {}
     for _ in range(a.rounds):
         for lib in a.libs:
-            path, _, opt = lib.partition(":")
+            spec, _, blocks = lib.partition("@")
+            path, _, opt = spec.partition(":")
             env = dict(os.environ, RASR_GMM_LIB=os.path.abspath(path), ROOT=ROOT, MODE=a.mode, FRAMES=str(frames),
                        STEPS=str(a.steps), DIM=str(a.dim), OPT=opt)
+            if blocks:
+                env["RASR_GMM_TARGET_BLOCKS"] = blocks
             p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 print(lib, "FAILED", p.stderr[-2000:])
