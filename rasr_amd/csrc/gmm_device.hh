@@ -66,6 +66,24 @@ __device__ __forceinline__ void lexMin(float& v, uint32_t& i, float v2, uint32_t
 // swaps x's odd 16-lane rows with y's even rows.  Taking min(x', y') afterwards leaves, in every
 // lane, the minimum over the lane and its partner (lane ^ 32, resp. lane ^ 16) of x in the lanes
 // that keep x and of y in the lanes that keep y: one swap + one min per exchanged pair.
+// Read-only per-launch tables (mixture tile offsets, mixture words) through the constant address space: a uniform
+// load from it is an s_load wherever it sits.  Through a generic pointer, a load after the kernel's own buffer stores
+// (the emit) cannot be proven unclobbered, so the compiler makes it a vector load plus v_readfirstlane and waits
+// s_waitcnt vmcnt(0) for it -- draining every tile load (or LDS-DMA) in flight at each mixture boundary.
+#ifndef GMM_CONST_TABLES
+#define GMM_CONST_TABLES 1
+#endif
+#if GMM_CONST_TABLES
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* constTable(const T* p) {
+    return (const __attribute__((address_space(4))) T*)p;
+}
+#else
+template <class T>
+__device__ __forceinline__ const T* constTable(const T* p) {
+    return p;
+}
+#endif
 __device__ __forceinline__ int swapMin32(int x, int y) {
     const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
     return min(static_cast<int>(r[0]), static_cast<int>(r[1]));

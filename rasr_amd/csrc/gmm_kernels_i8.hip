@@ -101,32 +101,45 @@ __device__ __forceinline__ void finalizeStoreI8(const I8Args& a, float* __restri
     const auto rb = __builtin_amdgcn_make_buffer_rsrc(bestOut ? bestOut + static_cast<size_t>(mo) * a.scoreStride
                                                               : nullptr,
                                                      (short)0, static_cast<int>(a.nFrames * 4u), 0x00020000);
+    // Both reference finalizes divide by b = 2 s^2: SimdFeatureScorer.cc:142 (f32)(0.5 * q / (f64)s2) and
+    // BatchFeatureScorer.cc:468 (f32)best / scale_ (scale_ = 2 s^2).  y = RN(x / b) from x (rh + rl) (1/b as two
+    // floats: within 2^-47 of x / b after one rounding, so a faithful quotient) and one Markstein correction
+    // (no special operands here: x a float integer, b a normal positive float).  batch: exactly the reference
+    // (x = (f32) best).  SIMD, |q| < 2^24: x = q; a quotient of two floats is never an f32 midpoint, and q / b
+    // is >= 2^-49 relative away from one, so the reference's double quotient (2^-53) rounds to the same f32.
+    // Larger |q| (never from a real mixture), and scales outside the range where this applies (finDivide),
+    // divide as the reference (tests/test_fastdiv_finalize.py: both in exact arithmetic).
+    // All NPL values take the multiply-and-correct path first, then ONE test decides the rare exact division (a
+    // test per value cost a branch and scalar mask juggling per value in the emit; -0.6 % batch-int, s24).
+    // ScaledContextScorer::score (ScaledFeatureScorer.hh:62-64): a finite score times 1.0f is itself, so the
+    // multiply is unconditional.
+    float sc[NPL];
+    int   qv[NPL];
+    bool  far = false;  // this lane holds a SIMD q outside +-2^24 (never from a real mixture)
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
-        const uint32_t f = frame0 + 64 * i + lane;
-        const int packed = res[i];
-        // mixture without densities: minScore stays Core::Type<int>::max
-        const bool     none = MAYBE_NONE && packed >= NONE_FROM;
-        const int      q    = none ? INT_MAX : (packed >> ib) + ssOut[i];
-        const uint32_t dns  = none ? 0xffffffffu : static_cast<uint32_t>(packed) & ((1u << ib) - 1u);
-        // Both reference finalizes divide by b = 2 s^2: SimdFeatureScorer.cc:142 (f32)(0.5 * q / (f64)s2) and
-        // BatchFeatureScorer.cc:468 (f32)best / scale_ (scale_ = 2 s^2).  y = RN(x / b) from x (rh + rl) (1/b as two
-        // floats: within 2^-47 of x / b after one rounding, so a faithful quotient) and one Markstein correction
-        // (no special operands here: x a float integer, b a normal positive float).  batch: exactly the reference
-        // (x = (f32) best).  SIMD, |q| < 2^24: x = q; a quotient of two floats is never an f32 midpoint, and q / b
-        // is >= 2^-49 relative away from one, so the reference's double quotient (2^-53) rounds to the same f32.
-        // Larger |q| (never from a real mixture), and scales outside the range where this applies (finDivide),
-        // divide as the reference (tests/test_fastdiv_finalize.py: both in exact arithmetic).
-        const float x = static_cast<float>(q), b = a.finB, r = a.finInv;
+        const int  packed = res[i];
+        const bool none   = MAYBE_NONE && packed >= NONE_FROM;  // no densities: Core::Type<int>::max
+        qv[i]             = none ? INT_MAX : (packed >> ib) + ssOut[i];
+        const float x = static_cast<float>(qv[i]), b = a.finB, r = a.finInv;
         const float y = __fmaf_rn(x, r, __fmul_rn(x, a.finInvLo));
-        float score   = __fmaf_rn(__fmaf_rn(-b, y, x), r, y);
-        if (a.finDivide != 0 || (a.flavor == 0 && static_cast<uint32_t>(q + (1 << 24)) >= (2u << 24)))
-            score = a.flavor == 0 ? static_cast<float>(0.5 * static_cast<double>(q) / static_cast<double>(a.s2))
-                                  : __fdiv_rn(x, a.batchScale);
-        // ScaledContextScorer::score (ScaledFeatureScorer.hh:62-64); a finite score times 1.0f is itself,
-        // so the multiply is unconditional (a select on the uniform test costs more than the multiply)
-        score = __fmul_rn(a.outScale, score);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rs, f * 4u, 0, GMM_STORE_CPOL);
+        sc[i]         = __fmaf_rn(__fmaf_rn(-b, y, x), r, y);
+        far           = far || static_cast<uint32_t>(qv[i] + (1 << 24)) >= (2u << 24);
+    }
+    if (a.finDivide != 0 || (a.flavor == 0 && far)) {
+#pragma unroll
+        for (int i = 0; i < NPL; ++i)
+            if (a.finDivide != 0 || static_cast<uint32_t>(qv[i] + (1 << 24)) >= (2u << 24))
+                sc[i] = a.flavor == 0 ? static_cast<float>(0.5 * static_cast<double>(qv[i]) / static_cast<double>(a.s2))
+                                      : __fdiv_rn(static_cast<float>(qv[i]), a.batchScale);
+    }
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const uint32_t f   = frame0 + 64 * i + lane;
+        const bool     none = MAYBE_NONE && res[i] >= NONE_FROM;
+        const uint32_t dns  = none ? 0xffffffffu : static_cast<uint32_t>(res[i]) & ((1u << ib) - 1u);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(__fmul_rn(a.outScale, sc[i])), rs, f * 4u, 0,
+                                              GMM_STORE_CPOL);
         if (bestOut)
             __builtin_amdgcn_raw_buffer_store_b32(dns, rb, f * 4u, 0, GMM_STORE_CPOL);
     }
@@ -343,8 +356,9 @@ constexpr int kSegTiles = GMM_I8_SEG;
 // preselection-batch-int: the segment ring and the waves' mask tables share one dynamic LDS array
 extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 
-// mixTileOff / scores / best are separate __restrict__ parameters so the mixture boundaries are read
-// with scalar loads (a vector load would need an s_waitcnt vmcnt(0) that drains the LDS-DMA queue).
+// The mixture boundaries and words are read through the constant address space (constTable, gmm_device.hh), so
+// they stay scalar loads after the emit's stores (a vector load would need an s_waitcnt vmcnt(0) that drains the
+// LDS-DMA queue).
 //
 // PRESEL (preselection-batch-int, NF = kI8PreselNF: 8, a wave's 128 frames are two 64-frame mask words; 4 kept
 // for A/B): keys are biased by 2^31
@@ -368,9 +382,11 @@ extern __shared__ __attribute__((aligned(16))) int8_t i8DynLds[];
 // (16 i + 4g + r >= er), and their candidates 2 v + p go to a second running minimum, merged at the mixture end.
 // A pair step holds two tiles of one kind.
 template <int NF, int KS, bool PRESEL = false, int SEG = kSegTiles, bool SCORE_ONLY = false, int W = 4>
-__global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W == 4) ? GMM_I8_WAVES : 1) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOff,
+__global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W == 4) ? GMM_I8_WAVES : 1) void scoreI8Seg(I8Args a, const uint32_t* __restrict__ mixTileOffArg,
                                                    float* __restrict__ scores, uint32_t* __restrict__ bestOut,
-                                                   const uint32_t* __restrict__ mixOddMask = nullptr) {
+                                                   const uint32_t* __restrict__ mixOddMaskArg = nullptr) {
+    const auto mixTileOff = constTable(mixTileOffArg);
+    const auto mixOddMask = constTable(mixOddMaskArg);
     static_assert(NF == 4 || NF == 8, "NF");
     static_assert(W == 4 || (W == 1 && !PRESEL), "waves per workgroup: 4, or 1 for small calls (no preselection)");
     static_assert(!PRESEL || NF == 4 || NF == 8, "preselection masks: one or two 64-frame words per wave");
@@ -888,6 +904,9 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
 #ifndef GMM_I8_PRESEL_WAVES
 #define GMM_I8_PRESEL_WAVES 3  // preselection: waves per SIMD the register allocation must allow
 #endif
+#ifndef GMM_I8_CLS_EARLYB
+#define GMM_I8_CLS_EARLYB 1  // score-only: every prologue load waited for before the loop (see scoreI8Cls)
+#endif
 #ifndef GMM_I8_CLS_DIAG
 #define GMM_I8_CLS_DIAG 0  // timing diagnostics only (wrong results): 1 = no per-mixture emit (the last one aside)
 #endif
@@ -899,9 +918,11 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
 // column block; the tile's epilogues follow its MFMAs in the same step (no pending tail).  A frame that selected
 // none of a mixture's densities keeps all ones: Core::Type<int>::max, as the reference.
 template <int NF, int SEG, int W, bool PRESEL = false>
-__global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : (NF == 16 ? 2 : 4)) : 1) void scoreI8Cls(I8Args a, const uint32_t* __restrict__ mixTileOff,
+__global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : (NF == 16 ? 2 : 4)) : 1) void scoreI8Cls(I8Args a, const uint32_t* __restrict__ mixTileOffArg,
                                                                                    float* __restrict__ scores,
-                                                                                   const uint32_t* __restrict__ mixWord) {
+                                                                                   const uint32_t* __restrict__ mixWordArg) {
+    const auto mixTileOff = constTable(mixTileOffArg);
+    const auto mixWord = constTable(mixWordArg);
     static_assert(NF == 4 || NF == 8 || (NF == 16 && !PRESEL), "NF");
     static_assert(!PRESEL || (NF == 8 && W == 4), "preselection: 128-frame waves (two 64-frame mask words)");
     constexpr int      LAG       = PRESEL ? 0 : GMM_I8_CLS_LAG;
@@ -976,6 +997,16 @@ __global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : (N
             if ((i * 64u + static_cast<uint32_t>(lane)) * 16u < words)
                 tabV[i] = src[i * 64 + lane];
     }
+    i32x4      B[NF];
+    int        ssOut[NPL];
+    const auto loadFrames = [&] {
+#pragma unroll
+        for (int cb = 0; cb < NF; ++cb)
+            B[cb] = reinterpret_cast<const i32x4*>(a.frameQ + static_cast<size_t>(frame0 + cb * 16 + (lane & 15)) * 64)[g];
+#pragma unroll
+        for (int i = 0; i < NPL; ++i)
+            ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
+    };
     if (nSeg > 0)
         issueSeg(0);
     if (nSeg > 1)
@@ -1012,16 +1043,14 @@ __global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : (N
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LUT and entries before the first segment's barrier
     }
 
-    i32x4 B[NF];
-#pragma unroll
-    for (int cb = 0; cb < NF; ++cb)
-        B[cb] = reinterpret_cast<const i32x4*>(a.frameQ + static_cast<size_t>(frame0 + cb * 16 + (lane & 15)) * 64)[g];
-    int ssOut[NPL];
-#pragma unroll
-    for (int i = 0; i < NPL; ++i)
-        ssOut[i] = a.frameSS[frame0 + 64 * i + lane];
-    if constexpr (PRESEL)  // every load before the ring (frame operands, table, the first segments) complete: the
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // waitcnt pass then leaves the loop without vmcnt waits (vmcnt(0))
+    loadFrames();
+    // Every load before the ring (frame operands, PRESEL's table, the first two segments) complete, by a real
+    // s_waitcnt vmcnt(0) the waitcnt pass sees: otherwise the frame operands and ssOut stay "pending" for it into the
+    // loops (it treats the counter as out of order while LDS-DMA is in flight, so no vmcnt(N) clears them), and it puts
+    // an s_waitcnt vmcnt(0) before every 2-tile iteration's first MFMA and in every emit -- each draining the DMA queue,
+    // i.e. waiting for the segment issued one segment ahead.  Here the wait costs the second segment's landing once.
+    if constexpr (PRESEL || GMM_I8_CLS_EARLYB)
+        __builtin_amdgcn_s_waitcnt(0x0f70);
 
     // mixture m ends at tile tEnd; its word wCur and the next mixture's end tNext are loaded one mixture ahead
     // (scalar loads whose latency the mixture's steps cover)

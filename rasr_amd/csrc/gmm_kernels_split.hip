@@ -1042,7 +1042,10 @@ __device__ __forceinline__ void emitMixtureSplitSum(const SplitArgs& a, const ui
 
 template <int KS, bool BEST>
 __global__ __launch_bounds__(kSplitFramesPerBlock / GMM_SPLIT_SUM_NF * 4, GMM_SPLIT_MIN_WAVES) void scoreSplitSum(
-        SplitArgs a, const uint32_t* __restrict__ mixTileOff) {
+        SplitArgs a, const uint32_t* __restrict__ mixTileOffArg) {
+    // mixture bounds through the constant address space (constTable): -2.1 % here (profiles/r05/s26); the other
+    // split kernels keep the generic pointer (the wide kernel neutral, scoreSplit32 +0.6 %, s27)
+    const auto mixTileOff = constTable(mixTileOffArg);
     constexpr int  NF   = GMM_SPLIT_SUM_NF;  // 4 or 8 column blocks; the emit works on halves of 4
     constexpr int  NH   = NF / 4;
     constexpr int  KH   = KS / 2;  // k-steps issued beside the first half of the epilogue
