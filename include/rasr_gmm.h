@@ -273,6 +273,15 @@ int gmm_scorer_kernel_time(gmm_scorer* scorer, double* total_ms, uint32_t* n_lau
  * copied into `data` (may be NULL to ask the size) -- or write it (the archive is created, or rewritten with its other
  * items kept).  GMM_ERR_INVALID_ARGUMENT if the file is not an archive of that format or has no such item.  Host
  * only; the preselection scorers use them for the item "density-clustering" (gmm_scorer_config.cache_archive). */
+/* Where a preselection scorer's density clustering came from (DensityClustering<F, D>::build,
+ * DensityClustering.tcc:122-155, which logs "using cached density clustering" / "density clustering written"):
+ * GMM_CLUSTERING_BUILT (built, not written: no or a read-only cache archive, or the write failed),
+ * GMM_CLUSTERING_WRITTEN (built and written to the cache archive), GMM_CLUSTERING_CACHED (read from it).
+ * GMM_ERR_UNSUPPORTED for a type without preselection. */
+#define GMM_CLUSTERING_BUILT 0
+#define GMM_CLUSTERING_WRITTEN 1
+#define GMM_CLUSTERING_CACHED 2
+int gmm_scorer_clustering_source(const gmm_scorer* scorer, int* source);
 int gmm_cache_archive_read_item(const char* path, const char* name, void* data, uint64_t capacity, uint64_t* size);
 int gmm_cache_archive_write_item(const char* path, const char* name, const void* data, uint64_t size);
 

@@ -165,6 +165,11 @@ GpuFeatureScorer::GpuFeatureScorer(const Core::Configuration& c, Core::Ref<const
     impl_ = Gpu::createFeatureScorer(ms, cfg, &err);
     if (!impl_)
         criticalError("GPU feature scorer: %s", err.c_str());
+    // DensityClustering<F, D>::build's messages (DensityClustering.tcc:127-154)
+    if (impl_->densityClusteringSource() == GMM_CLUSTERING_CACHED)
+        log("using cached density clustering");
+    else if (impl_->densityClusteringSource() == GMM_CLUSTERING_WRITTEN)
+        log("density clustering written");
     if (cfg.shardDevices.size() > 1)
         log("GPU feature scorer \"%s\" density-sharded over %zu devices, buffer size %u", scorerType,
             cfg.shardDevices.size(), cfg.bufferSize);

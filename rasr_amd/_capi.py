@@ -21,6 +21,7 @@ GMM_FLAG_REFERENCE_ORDER = 8  # diagonal-maximum / batch-float in the reference'
 GMM_FLAG_FULL_KEYS = 16  # batch-int / -fast: (score, density) keys instead of the score-only class layout
 GMM_FLAG_NO_SCORE_ONLY_TWIN = 32  # SIMD: no score-only copy of the model (callers that always want best densities)
 GMM_FLAG_CACHE_ARCHIVE_READ_ONLY = 64  # preselection: read the cached clustering, never write it
+GMM_CLUSTERING = {0: "built", 1: "written", 2: "cached"}  # gmm_scorer_clustering_source
 
 # Mm::Module_::FeatureScorerType values (src/Mm/Module.hh:48-70)
 BATCH_DIAGONAL_MAXIMUM_FLOAT = 0
@@ -141,6 +142,7 @@ PROTOTYPES = [
     ("gmm_scorer_density_clustering", ctypes.c_int,
      [ctypes.c_void_p, _u32p, _u32p, ctypes.c_void_p, ctypes.c_void_p]),
     ("gmm_scorer_cluster_selection", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("gmm_scorer_clustering_source", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     ("gmm_cache_archive_read_item", ctypes.c_int,
      [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     ("gmm_cache_archive_write_item", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64]),

@@ -221,7 +221,7 @@ struct gmm_scorer {
     // density table runs (gmm_score_device with best_density NULL, GMM_HOST_LAZY_BEST host calls): the
     // reference's score(e) without the index-carrying pack, bit-identical scores
     std::unique_ptr<gmm_scorer> scoresOnly;
-    bool clusteringCached = false;  // preselection: the clustering came from the cache archive
+    int clusteringSource = GMM_CLUSTERING_BUILT;  // preselection: built, built and written, or read from the archive
     // sparse best densities (gmm_best_density_pairs, gmm_kernels_pairs.hip): entry-major tables of the assigning
     // types in the reference's arithmetic; pairKind -1 where the model has none (e.g. float D > 128)
     int       pairKind = -1;
@@ -643,10 +643,12 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
         if (!err.empty())
             return fail(GMM_ERR_INVALID_ARGUMENT, err);
         // a write failure leaves the scorer as it is (the reference logs it and goes on)
-        if (!archive.empty() && !(s->cfg.flags & GMM_FLAG_CACHE_ARCHIVE_READ_ONLY))
-            (void)writeArchiveItem(archive, "density-clustering", encodeClusteringItem(s->clustering, nEntries));
+        if (!archive.empty() && !(s->cfg.flags & GMM_FLAG_CACHE_ARCHIVE_READ_ONLY) &&
+            writeArchiveItem(archive, "density-clustering", encodeClusteringItem(s->clustering, nEntries)))
+            s->clusteringSource = GMM_CLUSTERING_WRITTEN;
     }
-    s->clusteringCached = cached;
+    else
+        s->clusteringSource = GMM_CLUSTERING_CACHED;
     const DensityClustering& dc = s->clustering;
     const uint32_t           T  = static_cast<uint32_t>(rowEntry.size() / kTileRows);
     // per tile row: the byte offset of its cluster in a wave's mask table -- the float kernel's word table
@@ -2092,6 +2094,15 @@ int gmm_scorer_density_clustering(const gmm_scorer* s, uint32_t* nClusters, uint
         else
             std::copy(dc.meansF.begin(), dc.meansF.end(), static_cast<float*>(clusterMeans));
     }
+    return GMM_OK;
+}
+
+int gmm_scorer_clustering_source(const gmm_scorer* s, int* source) {
+    if (!s || !source)
+        return fail(GMM_ERR_INVALID_ARGUMENT, "null argument");
+    if (!s->presel)
+        return fail(GMM_ERR_UNSUPPORTED, "scorer type has no density preselection");
+    *source = s->clusteringSource;
     return GMM_OK;
 }
 

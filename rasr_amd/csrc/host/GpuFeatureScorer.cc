@@ -170,6 +170,11 @@ bool FeatureScorer::init(const MixtureSet& ms, const Configuration& c, uint32_t 
     return true;
 }
 
+int FeatureScorer::densityClusteringSource() const {
+    int source = -1;
+    return gmm_scorer_clustering_source(handle_, &source) == GMM_OK ? source : -1;
+}
+
 float FeatureScorer::inverseQuantizationFactor() const {
     float s = 0, q = 0;
     gmm_scorer_quantization(handle_, &s, &q);

@@ -159,6 +159,9 @@ public:
 
     // SimdGaussDiagonalMaximumFeatureScorer::inverseQuantizationFactor (SimdFeatureScorer.hh:128-130)
     float inverseQuantizationFactor() const;
+    // preselection types: where the density clustering came from (GMM_CLUSTERING_*, gmm_scorer_clustering_source);
+    // -1 for the other types
+    int densityClusteringSource() const;
     // SimdGaussDiagonalMaximumFeatureScorer::multiplyAndQuantize (SimdFeatureScorer.cc:37-52)
     std::vector<std::vector<uint8_t>> multiplyAndQuantize(const FeatureVector& f) const;
 

@@ -130,6 +130,13 @@ class Scorer:
                     "gmm_scorer_density_clustering")
         return coe, means
 
+    def clustering_source(self) -> str:
+        """Where the density clustering came from: "built", "written" (built and written to the cache archive) or
+        "cached" (read from it); gmm_scorer_clustering_source."""
+        v = ctypes.c_int()
+        _capi.check(self._lib.gmm_scorer_clustering_source(self._h, ctypes.byref(v)), "gmm_scorer_clustering_source")
+        return _capi.GMM_CLUSTERING[v.value]
+
     def cluster_selection(self, n_frames: int) -> np.ndarray:
         """The [n_frames][clusters] 0/1 selection of the last score call (synchronizes)."""
         n = ctypes.c_uint32()

@@ -120,6 +120,12 @@ int gmm_scorer_create_sharded(const gmm_mixture_set* m, gmm_scorer_type type, co
     return gmm_scorer_create(m, type, cfg, devices[0], out);
 }
 
+int gmm_scorer_clustering_source(const gmm_scorer* s, int* source) {
+    (void)s;
+    (void)source;
+    return fail(GMM_ERR_UNSUPPORTED, "stand-in: no preselection types");
+}
+
 int gmm_scorer_destroy(gmm_scorer* s) {
     delete s;
     return GMM_OK;

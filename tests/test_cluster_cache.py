@@ -167,6 +167,7 @@ def test_clustering_written_then_reused(gpu, tmp_path, kind):
     build_archive(p, [("lexicon-cache", b"keep me")])
     t = f"preselection-batch-{kind}"
     sc = ra.Scorer(ms, t, max_frames=200, clusters=64, select_clusters=8, cache_archive=p)
+    assert sc.clustering_source() == "written"
     coe, means = sc.density_clustering()
     items = dict(parse_archive(p))
     assert items["lexicon-cache"] == b"keep me"
@@ -185,6 +186,7 @@ def test_clustering_written_then_reused(gpu, tmp_path, kind):
     assert not np.array_equal(ref.cluster_of_entry, coe)
     cache_archive_write(p, ITEM, encode_clustering(kind, ref.dp, ref.cluster_of_entry, ref.cluster_means))
     sc = ra.Scorer(ms, t, max_frames=200, clusters=64, select_clusters=8, cache_archive=p)
+    assert sc.clustering_source() == "cached"
     coe2, means2 = sc.density_clustering()
     assert np.array_equal(coe2, ref.cluster_of_entry)
     assert np.array_equal(means2.view(np.uint8), ref.cluster_means.view(np.uint8))
@@ -202,6 +204,7 @@ def test_clustering_mismatch_rebuilds(gpu, tmp_path, kind):
     assert decode_clustering(dict(parse_archive(p))[ITEM])["clusters"] == 32
     # another cluster count: the item does not match (DensityClustering.cc:73-76) -> built and rewritten
     sc = ra.Scorer(ms, t, max_frames=64, clusters=48, select_clusters=4, cache_archive=p)
+    assert sc.clustering_source() == "written"
     ref = oracle.OraclePresel(ms, kind, clusters=48, select=4)
     coe, means = sc.density_clustering()
     assert np.array_equal(coe, ref.cluster_of_entry)
@@ -218,6 +221,7 @@ def test_clustering_mismatch_rebuilds(gpu, tmp_path, kind):
                  encode_clustering(kind, ref.dp, ref.cluster_of_entry, ref.cluster_means)[:-5]):
         cache_archive_write(p, ITEM, blob)
         sc = ra.Scorer(ms, t, max_frames=64, clusters=48, select_clusters=4, cache_archive=p)
+        assert sc.clustering_source() == "written"
         coe, _ = sc.density_clustering()
         assert np.array_equal(coe, ref.cluster_of_entry)
         sc.close()
@@ -232,10 +236,18 @@ def test_clustering_read_only_archive(gpu, tmp_path):
     p = str(tmp_path / "ro.cache")
     sc = ra.Scorer(ms, "preselection-batch-int", max_frames=64, clusters=16, select_clusters=4, cache_archive=p,
                    cache_archive_read_only=True)
+    assert sc.clustering_source() == "built"
     sc.close()
     assert not os.path.exists(p)  # built, not written
     ref = oracle.OraclePresel(ms, "int", clusters=16, select=4, iterations=2)
     build_archive(p, [(ITEM, encode_clustering("int", ref.dp, ref.cluster_of_entry, ref.cluster_means))])
     sc = ra.Scorer(ms, "preselection-batch-int", max_frames=64, clusters=16, select_clusters=4, cache_archive=p,
                    cache_archive_read_only=True)
+    assert sc.clustering_source() == "cached"
     assert np.array_equal(sc.density_clustering()[0], ref.cluster_of_entry)  # read
+    sc.close()
+    # no archive: built; a type without preselection has no clustering
+    assert ra.Scorer(ms, "preselection-batch-int", max_frames=64, clusters=16,
+                     select_clusters=4).clustering_source() == "built"
+    with pytest.raises(ra._capi.GmmError):
+        ra.Scorer(ms, "batch-diagonal-maximum-int", max_frames=64).clustering_source()
