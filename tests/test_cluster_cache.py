@@ -132,6 +132,10 @@ def test_archive_errors(built, tmp_path):
     with open(p, "ab") as f:  # a truncated item ends the list (MappedArchive::loadData)
         f.write(struct.pack("<IQ", 1, 99) + b"t")
     assert cache_archive_read(p, "x") == b"1"
+    with pytest.raises(ra._capi.GmmError):  # an archive that cannot be written (missing directory)
+        cache_archive_write(str(tmp_path / "no-such-dir" / "a.cache"), "x", b"1")
+    with pytest.raises(ra._capi.GmmError):  # an empty item name (MappedArchive::loadData rejects name length 0)
+        cache_archive_write(p, "", b"1")
 
 
 def test_cache_archive_config_field(built):
