@@ -286,12 +286,18 @@ int main(int argc, char** argv) {
     if (const char* sd = std::getenv("RASR_DRIVER_SHARD_DEVICES"))
         for (uint32_t d : parseList(sd))
             cfg.shardDevices.push_back(static_cast<int>(d));
+    // RASR_DRIVER_CACHE_ARCHIVE=path: the density clustering's cache archive (preselection types); the driver reports
+    // where the clustering came from on stderr ("clustering: built|written|cached")
+    if (const char* ca = std::getenv("RASR_DRIVER_CACHE_ARCHIVE"))
+        cfg.cacheArchive = ca;
     std::string                             err;
     std::unique_ptr<Mm::Gpu::FeatureScorer> scorer = Mm::Gpu::createFeatureScorer(ms, cfg, &err);
     if (!scorer) {
         fprintf(stderr, "createFeatureScorer failed: %s\n", err.c_str());
         return 3;
     }
+    if (const int src = scorer->densityClusteringSource(); src >= 0)
+        fprintf(stderr, "clustering: %s\n", src == GMM_CLUSTERING_CACHED ? "cached" : src == GMM_CLUSTERING_WRITTEN ? "written" : "built");
     const uint32_t        M = scorer->nMixtures();
     std::vector<float>    outS;
     std::vector<uint32_t> outB;

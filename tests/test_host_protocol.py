@@ -27,7 +27,8 @@ def _write_model(path, ms):
         ms.mixture_log_weights.astype(np.float64).tofile(f)
 
 
-def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, protocol="recognizer", shard_devices=None):
+def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, protocol="recognizer", shard_devices=None,
+         cache_archive=None, stderr_out=None):
     mp, fp, op = tmp_path / "m.drvmodel", tmp_path / "f.bin", tmp_path / "o.bin"
     if model_file is None:
         _write_model(mp, ms)
@@ -39,8 +40,12 @@ def _run(tmp_path, ms, frames, kind, buffer_size, segments, model_file=None, pro
     env = dict(os.environ)
     if shard_devices:
         env["RASR_DRIVER_SHARD_DEVICES"] = ",".join(str(d) for d in shard_devices)
-    subprocess.run([DRIVER, str(mp), str(fp), str(op), kind, str(buffer_size), str(segments), protocol], check=True,
-                   timeout=300, env=env)
+    if cache_archive:
+        env["RASR_DRIVER_CACHE_ARCHIVE"] = str(cache_archive)
+    r = subprocess.run([DRIVER, str(mp), str(fp), str(op), kind, str(buffer_size), str(segments), protocol], check=True,
+                       timeout=300, env=env, stderr=subprocess.PIPE, text=True)
+    if stderr_out is not None:
+        stderr_out.append(r.stderr)
     raw = np.fromfile(op, dtype=np.uint32)
     F, M, launches = raw[:3]
     s = raw[3:3 + F * M].view(np.float32).reshape(F, M)
@@ -144,6 +149,23 @@ def test_preselection_protocol(gpu, tmp_path, kind):
     else:
         err = np.abs(s.T.astype(np.float64) - ref) / np.maximum(1, np.abs(ref))
         assert err.max() <= 1e-4
+
+
+@pytest.mark.gpu
+def test_preselection_cache_archive_protocol(gpu, tmp_path):
+    # Gpu::Configuration::cacheArchive (the adapter's "density-clustering.cache-archive"): the first drop-in scorer
+    # builds and writes the clustering, the second reads it -- same scores, bit-exact against the oracle
+    ms = ra.synthetic_mixture_set(40, 12, 39, seed=47, weights="random")
+    frames = ra.synthetic_frames(37, 39, seed=48)
+    archive = tmp_path / "global.cache"
+    err = []
+    s1, _, _ = _run(tmp_path, ms, frames, "preselection-batch-int", 4, 2, cache_archive=archive, stderr_out=err)
+    s2, _, _ = _run(tmp_path, ms, frames, "preselection-batch-int", 4, 2, cache_archive=archive, stderr_out=err)
+    assert "clustering: written" in err[0] and "clustering: cached" in err[1], err
+    assert archive.exists()
+    ref = oracle.OraclePresel(ms, "int").score(frames)
+    assert np.array_equal(s1.T.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(s2.view(np.uint32), s1.view(np.uint32))
 
 
 @pytest.mark.gpu
