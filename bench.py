@@ -951,7 +951,7 @@ def fenced_extras(args, ws: int, rank: int, guard: LineGuard, group) -> None:
 def make_line(args, res, ws: int) -> dict:
     n_dens = args.mixtures * args.densities
     return {
-        "metric": "frames/sec scored, 39-dim x 800k-density diag-GMM",
+        "metric": f"frames/sec scored, {args.dim}-dim x {n_dens // 1000}k-density diag-GMM",
         "value": res["value"],
         "unit": "frames/s",
         "n_gpus": ws,

@@ -222,6 +222,8 @@ struct gmm_scorer {
     // reference's score(e) without the index-carrying pack, bit-identical scores
     std::unique_ptr<gmm_scorer> scoresOnly;
     int clusteringSource = GMM_CLUSTERING_BUILT;  // preselection: built, built and written, or read from the archive
+    // the caller's cache_archive string is only valid during create: keep a copy, and cfg.cache_archive stays null
+    std::string cacheArchive;
     // sparse best densities (gmm_best_density_pairs, gmm_kernels_pairs.hip): entry-major tables of the assigning
     // types in the reference's arithmetic; pairKind -1 where the model has none (e.g. float D > 128)
     int       pairKind = -1;
@@ -630,7 +632,7 @@ int setupPreselection(gmm_scorer* s, const gmm_mixture_set& ms, const void* entr
     const uint32_t nEntries = ms.mixture_offsets[ms.n_mixtures];
     // DensityClustering::build (DensityClustering.tcc:122-155): the cached clustering if the archive holds a matching
     // one, else build it and cache it
-    const std::string archive = s->cfg.cache_archive ? s->cfg.cache_archive : "";
+    const std::string& archive = s->cacheArchive;
     std::vector<char> item;
     const uint32_t    nClusters = std::min(s->cfg.clusters, nEntries);  // "reducing number of clusters", cc:51-54
     const bool        cached    = !archive.empty() && nEntries > 0 && s->cfg.select_clusters >= 1 &&
@@ -1352,6 +1354,8 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
     s->quantized = quantized;
     s->device   = device;
     s->cfg      = cfg;
+    s->cacheArchive      = cfg.cache_archive ? cfg.cache_archive : "";
+    s->cfg.cache_archive = nullptr;
     s->D        = ms->dimension;
     s->C        = ms->n_covariances;
     s->nFramesPad = (cfg.max_frames + kFramePadQuantum - 1) / kFramePadQuantum * kFramePadQuantum;

@@ -13,7 +13,7 @@
 //     direct scorer (gmm_kernels_direct.hip: four lane sums over 4-dimension blocks, pairwise, then the D % 4
 //     tail), the f64 three-term score, the f32-stored best replaced when (f64) best > score;
 //   * diagonal-sum (GaussDiagonalMaximumFeatureScorer.cc:238-286): the same distance, the f32 score
-//     0.5 ((dist + w) + logNorm), the minimum by a strict f32 compare.
+//     0.5 ((w + logNorm) + dist), the minimum by a strict f32 compare.
 // The keyed table scorers compute the float types' best densities on the split-f16 MFMA path; on a near tie
 // (scores within the float tolerance) the two may name different densities, as either may differ from the
 // CPU restatement (tests/test_best_pairs.py).
@@ -91,15 +91,18 @@ __global__ __launch_bounds__(256) void bestPairs(PairArgs a) {
                 }
                 else if constexpr (KIND == kPairDiagonalMaximum) {
                     const float  r = refDistance(a, x, i, cov);
-                    const double s = __dadd_rn(__dadd_rn(static_cast<double>(r), static_cast<double>(a.fConst[i])),
-                                               static_cast<double>(a.fLogNorm[cov]));
+                    // GDMFS.cc:129-132: ((f64) w + (f64) logNorm) + (f64) distance
+                    const double s = __dadd_rn(__dadd_rn(static_cast<double>(a.fConst[i]),
+                                                         static_cast<double>(a.fLogNorm[cov])),
+                                               static_cast<double>(r));
                     const uint64_t b = static_cast<uint64_t>(__double_as_longlong(s));
                     v0               = static_cast<uint32_t>(b);
                     v1               = static_cast<uint32_t>(b >> 32);
                 }
                 else {
                     const float r = refDistance(a, x, i, cov);
-                    const float s = __fadd_rn(__fadd_rn(r, a.fConst[i]), a.fLogNorm[cov]);
+                    // GDMFS.cc:255-257: (w + logNorm) + distance in f32
+                    const float s = __fadd_rn(__fadd_rn(a.fConst[i], a.fLogNorm[cov]), r);
                     v0            = __float_as_uint(__fmul_rn(0.5f, s));
                 }
             }

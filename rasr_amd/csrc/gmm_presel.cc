@@ -266,7 +266,11 @@ bool readArchiveItem(const std::string& path, const std::string& name, std::vect
 bool writeArchiveItem(const std::string& path, const std::string& name, const std::vector<char>& data) {
     std::vector<ArchiveItem> items;
     (void)readArchive(path, items);  // keep the archive's other items (a missing or foreign file starts empty)
-    const std::string tmp = path + ".temp." + std::to_string(static_cast<long>(getpid()));
+    // MappedArchive.cc:40-48, 114: "<archive>.temp.<host>.<pid>" -- archives may sit on a shared filesystem
+    char host[256] = {0};
+    if (gethostname(host, sizeof(host) - 1) != 0)
+        std::strcpy(host, "unknown");
+    const std::string tmp = path + ".temp." + host + "." + std::to_string(static_cast<long>(getpid()));
     {
         std::ofstream out(tmp, std::ios::binary | std::ios::trunc);
         if (!out)

@@ -332,11 +332,13 @@ Scorer GpuFeatureScorer::getScorer(const FeatureVector& f) const {
 
 DensityInMixture GpuFeatureScorer::slotBestDensity(Slot& slot, EmissionIndex e) const {
     bestEager_ = true;  // from the next getScorer() on, the calls compute best densities too
+    // an emission answered alone keeps that answer for this frame, also after the whole table was fetched
+    // (the reference memoizes per (frame, emission), AssigningFeatureScorer.hh:110-121)
+    for (const auto& kv : slot.sparse)
+        if (kv.first == e)
+            return kv.second;
     if (!slot.bestValid) {
         // the asked emission alone, while the frame is still on the device (its call is the newest)
-        for (const auto& kv : slot.sparse)
-            if (kv.first == e)
-                return kv.second;
         uint32_t pos = 0, v = 0;
         if (slot.sparse.size() < kSparseMax && gmm_best_density_pairs(handle_, slot.call, &pos, &e, 1, &v) == GMM_OK) {
             ++bestPairs_;
@@ -554,6 +556,11 @@ DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t
     if (!cached_[p])
         fill(featureIndex, length, true);
     const size_t o = static_cast<size_t>(p) * rowStride() + e;
+    // a pair answered alone for this frame keeps its answer (memoized as the reference's context scorer does)
+    const uint64_t key = (static_cast<uint64_t>(p) << 32) | e;
+    const auto     it  = sparse_.find(key);
+    if (it != sparse_.end() && it->second.first == generation_[p])
+        return it->second.second;
     if (bestCached_[p])
         return best_[o];
     // a position of a score-only call (made before the first bestDensity()): the asked pair alone while that
@@ -562,18 +569,15 @@ DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t
     if (call != sparseCall_) {
         sparseCall_  = call;
         sparseAsked_ = 0;
-        sparse_.clear();
+        for (auto i = sparse_.begin(); i != sparse_.end();)  // answers of frames no longer buffered
+            i = i->second.first == generation_[i->first >> 32] ? std::next(i) : sparse_.erase(i);
     }
-    const uint64_t key = (static_cast<uint64_t>(p) << 32) | e;
-    const auto     it  = sparse_.find(key);
-    if (it != sparse_.end())
-        return it->second;
     if (sparseAsked_ < kSparseMax) {
         uint32_t pos = p, v = 0;
         if (gmm_best_density_pairs(handle_, call, &pos, &e, 1, &v) == GMM_OK) {
             ++sparseAsked_;
             ++bestPairs_;
-            sparse_.emplace(key, v);
+            sparse_[key] = {generation_[p], v};
             return v;
         }
     }

@@ -295,7 +295,10 @@ private:
     // the score-only call whose pairs were answered one by one, how many, and the answers (key position << 32 | e)
     mutable uint64_t          sparseCall_ = 0;
     mutable uint32_t          sparseAsked_ = 0;
-    mutable std::unordered_map<uint64_t, DensityInMixture> sparse_;
+    // answers of single (position, e) pairs, with the position's generation: once answered, a pair keeps its
+    // answer for that frame (CachedAssigningContextScorer memoizes, AssigningFeatureScorer.hh:110-121), even after
+    // the position's whole table was fetched in the keyed scorer's arithmetic
+    mutable std::unordered_map<uint64_t, std::pair<uint32_t, DensityInMixture>> sparse_;
     mutable int32_t           currentFeature_ = 0;
     mutable int32_t           buffered_       = 0;
     mutable uint32_t          launches_       = 0, bestFetches_ = 0, bestPairs_ = 0;

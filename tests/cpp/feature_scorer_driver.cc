@@ -228,14 +228,19 @@ int main(int argc, char** argv) {
     if (argc >= 2 && std::string(argv[1]) == "bench")
         return benchMain(argc, argv);
     if (argc != 7 && argc != 8) {
-        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node|delayed|search|late|aligner]\n",
+        fprintf(stderr, "usage: %s model.bin frames.bin out.bin type bufferSize segments [recognizer|node|delayed|search|late|aligner|memo]\n",
                 argv[0]);
         return 2;
     }
     const std::string protocol = argc == 8 ? argv[7] : "recognizer";
     if (protocol != "recognizer" && protocol != "node" && protocol != "delayed" && protocol != "search" &&
-        protocol != "late" && protocol != "aligner")
+        protocol != "late" && protocol != "aligner" && protocol != "memo")
         return 2;
+    // the reference memoizes bestDensity(e) per (frame, e) (AssigningFeatureScorer.hh:110-121): "memo" asks
+    // bestDensity(0) first, then every other emission (past the drop-in's kSparseMax single-pair answers), then
+    // bestDensity(0) again; output: the first answer of each emission; stderr: "memo mismatches: N" (second != first)
+    const bool memo = protocol == "memo";
+    uint32_t   memoMismatches = 0;
     const bool search = protocol == "search";  // the recognizer's sequence, score(e) only (no bestDensity)
     const bool late   = protocol == "late";    // score(e) only for the first half of the frames, then bestDensity too
     // an aligner's read (AbstractMixtureSetEstimator.cc:370-384): score(e) of every emission, bestDensity(e) of 1-10
@@ -307,7 +312,15 @@ int main(int argc, char** argv) {
         const size_t   row      = outB.size();
         for (uint32_t e = 0; e < n; ++e) {
             outS.push_back(node ? -s->score(e) : s->score(e));  // FeatureScorerNode::putData: +log space
-            outB.push_back(readBest && !aligner ? s->bestDensity(e) : 0xffffffffu);
+            outB.push_back(readBest && !aligner && !memo ? s->bestDensity(e) : 0xffffffffu);
+        }
+        if (memo && readBest) {
+            const Mm::Gpu::DensityInMixture first = s->bestDensity(0);
+            outB[row]                    = first;
+            for (uint32_t e = 1; e < n; ++e)
+                outB[row + e] = s->bestDensity(e);
+            if (s->bestDensity(0) != first)
+                ++memoMismatches;
         }
         if (aligner && readBest) {
             Rng pick{0x5eedull + consumed};
@@ -351,6 +364,8 @@ int main(int argc, char** argv) {
             scorer->reset();
         }
     }
+    if (memo)
+        fprintf(stderr, "memo mismatches: %u\n", memoMismatches);
     uint32_t launches = 0;
     if (auto* b = dynamic_cast<Mm::Gpu::GpuBatchFeatureScorer*>(scorer.get()))
         launches = b->nLaunches();

@@ -337,3 +337,31 @@ def test_aligner_sparse_best_densities(gpu, tmp_path, kind, buffer_size):
         ref_s, ref_b = of.score(frames)[:2]
         assert (np.abs(s.T.astype(np.float64) - ref_s) / np.maximum(1, np.abs(ref_s))).max() <= 1e-4
         _near_tie_ok(ms, frames.astype(np.float64), b, ref_b, asked)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,buffer_size", [("diagonal-maximum", 1), ("diagonal-maximum", 8), ("diagonal-sum", 8)])
+def test_best_density_memoized_across_table_switch(gpu, tmp_path, kind, buffer_size):
+    """bestDensity(e) of one (frame, e) is answered once (the reference's
+    CachedAssigningContextScorer memoizes it, AssigningFeatureScorer.hh:110-121).  Mixture 0 holds a planted near tie
+    -- two densities with the same mean, the second better by 1e-4 in -2 log c, below the keyed table's resolution
+    but above f32's -- so the single-pair answer (the reference's arithmetic: density 1) and the keyed table's
+    differ.  The consumer asks bestDensity(0), then every other emission (past kSparseMax single-pair answers: the
+    call's whole keyed table is fetched), then bestDensity(0) again: both answers are the same, and the first frame's
+    is the reference's."""
+    ms = ra.synthetic_mixture_set(40, 4, 39, seed=69, weights="random")
+    ms.means[1] = ms.means[0]
+    lw = np.log(0.25)
+    ms.mixture_log_weights[:4] = [lw, lw + 5e-5, np.log(0.3), np.log(0.2) - 1e-2]
+    frames = ra.synthetic_frames(24, 39, seed=70)
+    err = []
+    s, b, _ = _run(tmp_path, ms, frames, kind, buffer_size, 1, protocol="memo", stderr_out=err)
+    assert "memo mismatches: 0" in err[0], err[0]
+    of = oracle.OracleFloatSum(ms) if kind == "diagonal-sum" else oracle.OracleFloat(ms)
+    ref_b = of.score(frames)[1]
+    assert (ref_b[0] == 1).all()  # the planted tie: the reference names density 1
+    assert b[0, 0] == 1
+    # the keyed table (what the fetched table holds) names density 0 for this tie: the memo is what kept the answer
+    sc = ra.Scorer(ms, kind, max_frames=24)
+    assert (sc.score_host(frames)[1][0] == 0).any()
+    assert (b != 0xFFFFFFFF).all()
