@@ -311,14 +311,14 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         d_local = int(ms.n_entries)
     algo = 2.0 * args.dim * d_local * fpl  # one multiply-add per (frame, density, component), per launch
     kernel = sc.main_kernel()
-    split = kernel in ("scoreSplit", "scoreSplitWide", "scoreSplit32", "scoreSplitSum")
+    split = kernel in ("scoreSplit", "scoreSplitWide", "scoreSplit32", "scoreSplitSum", "scoreSplit32Sum")
     if split:
         # f32-accurate contraction on the f16 matrix cores: 3 f16 products per f32 multiply-add, so the
         # roofline for this arithmetic is the dense f16 peak / 3; the MFMA work actually issued covers
         # K = 3 D + 7 (row-constant and ||x'||^2 limbs) padded to the K step (32 for 16x16x32, 16 for
         # 32x32x16) per (frame, density)
         peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PRODUCTS
-        kq = 16 if kernel == "scoreSplit32" else 32
+        kq = 16 if kernel in ("scoreSplit32", "scoreSplit32Sum") else 32
         k_issued = kq * ((3 * args.dim + 7 + kq - 1) // kq)
         issued = 2.0 * k_issued * d_local * fpl
     elif mode in ("fp32", "fp32-scores", "sum"):
@@ -359,6 +359,19 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
             "output_bytes_per_launch": m_local * fpl * (4 + (0 if best is None else 4)),
         },
     }
+    if kernel in ("scoreSplitSum", "scoreSplit32Sum"):
+        # diagonal-sum's epilogue is VALU issue-bound: per (frame, density) v_fma + v_exp_f32 + v_add_f32 (4 + 8 + 4
+        # cycles per wave64 instruction), the key v_and_or_b32 (4) and half a v_min3 (2) with best densities, plus
+        # the cycles the MFMAs hold the vector issue (8 per 32x32x16 over 16 K: 4 per 64 values at K = 128; 8 per
+        # 16x16x32 over 32 K: 8 per 64 values)
+        cyc = (16 + (6 if best is not None else 2)) + (4 if kernel == "scoreSplit32Sum" else 8)
+        ceiling = N_SIMDS * CLOCK_GHZ * 1e9 * 64.0 / (cyc * d_local)
+        res["roofline"]["valu"] = {
+            "ceiling_frames_per_s": ceiling,
+            "frac": (fpl / sec) / ceiling,
+            "basis": f"{cyc} issue cycles per 64 (frame, density) values per SIMD (MI355X_MICROARCH.md issue costs), "
+                     f"{N_SIMDS} SIMDs at {CLOCK_GHZ} GHz",
+        }
     if kernel.startswith("scoreI8"):
         # the quantized scorer is reported against max(t_MFMA, t_VALU).  Its epilogue is one
         # 3-source VOP3 (v_lshl_add) per (frame, density) plus half a v_min3; a wave64 VOP3 issues every

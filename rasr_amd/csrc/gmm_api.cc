@@ -351,7 +351,8 @@ int chunkTableFor(gmm_scorer* s, uint32_t nFrameTiles, const ChunkTable** out) {
     const uint32_t kTargetBlocks =
             kOverride ? kOverride
             : s->split ? std::clamp<uint32_t>(nFrameTiles * 256u, 1024u,
-                                              s->flavor == Flavor::DiagonalSum ? uint32_t(GMM_TARGET_BLOCKS)  // 64-frame waves:
+                                              s->flavor == Flavor::DiagonalSum && s->splitRows == 16
+                                                      ? uint32_t(GMM_TARGET_BLOCKS)  // 64-frame waves:
                                                                                : uint32_t(GMM_SPLIT_TARGET_BLOCKS))  // 8192 (A/B)
             : s->quantized && !s->presel ? std::clamp<uint32_t>(nFrameTiles * 1024u, 2048u, uint32_t(GMM_TARGET_BLOCKS))
                                          : uint32_t(GMM_TARGET_BLOCKS);
@@ -549,7 +550,7 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         TimedSpan span(s, stream);
         GMM_HIP_CHECK(span.begin());
         if (s->flavor == Flavor::DiagonalSum)
-            GMM_HIP_CHECK(launchScoreSplitSum(a, s->kSteps16, stream));
+            GMM_HIP_CHECK(launchScoreSplitSum(a, s->splitRows, s->kSteps16, stream));
         else
             GMM_HIP_CHECK(launchScoreSplit(a, s->splitRows, s->kSteps16, stream));
         GMM_HIP_CHECK(span.end());
@@ -2011,7 +2012,7 @@ int gmm_scorer_launch_info(const gmm_scorer* s, uint32_t nFrames, uint32_t* nLau
     if (nLaunches)
         *nLaunches = s->presel ? 3 : 2;
     if (name)
-        *name = s->quantized ? "scoreI8" : s->direct ? "scoreDirect" : (s->split ? (s->flavor == Flavor::DiagonalSum ? "scoreSplitSum"
+        *name = s->quantized ? "scoreI8" : s->direct ? "scoreDirect" : (s->split ? (s->flavor == Flavor::DiagonalSum ? (s->splitRows == 32 ? "scoreSplit32Sum" : "scoreSplitSum")
                                                                          : (s->splitRows == 32 ? "scoreSplit32" : (splitWideOf(s) ? "scoreSplitWide" : "scoreSplit")))
                                                        : "scoreF32");
     return GMM_OK;

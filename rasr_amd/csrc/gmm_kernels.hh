@@ -177,7 +177,7 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream);
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps, hipStream_t stream);
-hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps, hipStream_t stream);  // diagonal-sum, 16-row tiles
+hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t rows, uint32_t kSteps, hipStream_t stream);  // diagonal-sum
 constexpr uint32_t kSplit32MaxKSteps = 10;  // 32-row split kernel instantiated for K/16 <= 10 (D <= 51)
 hipError_t launchScoreI8(const I8Args& a, uint32_t kSteps, bool multiCov, hipStream_t stream);
 

@@ -1289,6 +1289,238 @@ __global__ __launch_bounds__(kSplitFramesPerBlock / GMM_SPLIT_SUM_NF * 4, GMM_SP
     }
 }
 
+// ---------------------------------------------------------------------------
+// diagonal-sum on 32-row tiles (v_mfma_f32_32x32x16_f16; round 6).  The sum's epilogue is VALU-bound: per
+// value a key (v_and_or_b32), half a v_min3, and v_fma + v_exp_f32 + v_add_f32 for the exponential sum, about 23
+// issue cycles, where diagonal-maximum needs 6.  A 16x16x32 MFMA holds the SIMD's vector issue for 8 of its 16
+// cycles, a 32x32x16 one for 8 of its 32, so per unit of matrix work the 32-row shape leaves 1.5x the issue
+// cycles to that epilogue (MI355X_MICROARCH.md, the issue-cost row).  Layout and keys are scoreSplit32's: a
+// wave holds 4 column blocks of 32 frames (128 frames, f16 fragments in the AGPRs), lane l owns frame l & 31 of a
+// block and rows (i & 3) + 8 (i >> 2) + 4 (l >> 5) in its accumulator registers i; keys carry (tile << 4 | i).
+// Exponential sum (as scoreSplitSum): exp(-s_d) = exp(K0/2) 2^(-kap u_d) with kap = 0.5 log2(e) 2^e of the frame;
+// per lane and block a reference R and S = sum 2^(R - kap u).  R follows the running minimum every tile without a
+// branch (online rescale: R' = min(R, kap min u), S *= 2^(R' - R)), so every exponent is <= 0.  Padding rows carry
+// a 2^29 constant bias (gmm_prepare.cc): their exponentials underflow to 0 and their keys never win.
+// ---------------------------------------------------------------------------
+template <bool BEST>
+__device__ __forceinline__ void emitMixtureSplit32Sum(const SplitArgs& a, const uint32_t (&best)[2][2],
+                                                      const float (&S)[2][2], const float (&R)[2], uint32_t m,
+                                                      uint32_t frame0, int lane, uint32_t kmask) {
+    uint32_t k[2];
+    float    sum[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        k[b]   = min(best[b][0], best[b][1]);
+        sum[b] = S[b][0] + S[b][1];
+    }
+    // lanes < 32 keep block 0, lanes >= 32 block 1; [0] from lane half h = 0 (rows 4h ..), [1] from h = 1
+    const auto r  = __builtin_amdgcn_permlane32_swap(k[0], k[1], false, false);
+    const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(R[0]), __float_as_uint(R[1]), false, false);
+    const auto rs = __builtin_amdgcn_permlane32_swap(__float_as_uint(sum[0]), __float_as_uint(sum[1]), false, false);
+    const uint32_t hi0 = r[0] & ~15u, hi1 = r[1] & ~15u;
+    const uint32_t row0 = (r[0] & 3u) | ((r[0] & 12u) << 1), row1 = ((r[1] & 3u) | ((r[1] & 12u) << 1)) + 4u;
+    const bool     take = BEST ? (hi1 < hi0 || (hi1 == hi0 && row1 < row0)) : r[1] < r[0];
+    const uint32_t key  = take ? r[1] : r[0];
+    const uint32_t row  = take ? row1 : row0;
+    // merge the two halves' (R, S) on the smaller R
+    const float ra = __uint_as_float(rr[0]), rb = __uint_as_float(rr[1]);
+    const float sa = __uint_as_float(rs[0]), sb = __uint_as_float(rs[1]);
+    const float d  = ra - rb;
+    const float rf = fminf(ra, rb);
+    const float sf = d <= 0.0f ? __builtin_fmaf(sb, __builtin_amdgcn_exp2f(d), sa)
+                               : __builtin_fmaf(sa, __builtin_amdgcn_exp2f(-d), sb);
+
+    const float kv   = __uint_as_float((key & ~kmask) | ((kmask + 1u) >> 1));
+    const bool  none = !(kv < 1e37f);  // empty mixture: R stays 1e30, S = 0 -> +inf, as the reference
+    // -log sum exp(-s_d) = R ln2 - K0/2 - ln S
+    const float score = __fmul_rn(a.outScale, (rf - __builtin_amdgcn_logf(sf)) * 0.693147181f - 0.5f * a.offsetK0);
+    const uint32_t idx = none ? 0xffffffffu : ((((key & kmask) >> 4) << 5) | row);
+    const uint32_t mo  = m - a.mixBase;
+    const uint32_t off = static_cast<uint32_t>(frame0 + lane) * 4u;
+    const auto rsS = __builtin_amdgcn_make_buffer_rsrc(a.scores + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                      static_cast<int>(a.nFrames * 4u), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(score), rsS, off, 0, GMM_STORE_CPOL);
+    if constexpr (BEST) {
+        const auto rb_ = __builtin_amdgcn_make_buffer_rsrc(a.best + static_cast<size_t>(mo) * a.scoreStride, (short)0,
+                                                          static_cast<int>(a.nFrames * 4u), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(idx, rb_, off, 0, GMM_STORE_CPOL);
+    }
+}
+
+#ifndef GMM_SPLIT32_SUM_IL
+#define GMM_SPLIT32_SUM_IL 10  // VALU per MFMA in the interleave of a step (the epilogue's ~316 VALU beside 32 MFMAs)
+#endif
+
+template <int KS, bool BEST>
+__global__ __launch_bounds__(64 * (kSplitFramesPerBlock / 128), 1) void scoreSplit32Sum(
+        SplitArgs a, const uint32_t* __restrict__ mixTileOffArg) {
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    const auto    mixTileOff = constTable(mixTileOffArg);
+    constexpr int NB = 4, NH = 2;  // blocks of 32 frames; halves of 64 frames (one emit each)
+    const int     lane = threadIdx.x & 63;
+    const int     wave = threadIdx.x >> 6;
+    uint32_t      chunk, ft;
+    if (!mapBlock(a.nChunks, a.nFrameTiles, chunk, ft))
+        return;
+    const uint32_t frame0 = ft * kSplitFramesPerBlock + static_cast<uint32_t>(wave) * (32u * NB);
+    const uint32_t fb0    = frame0 / 32u;
+    const uint32_t m0 = a.chunkMixOff[chunk], m1 = a.chunkMixOff[chunk + 1];
+    const uint32_t T0 = mixTileOff[m0], T1 = mixTileOff[m1];
+
+    const f16x8* th       = static_cast<const f16x8*>(a.tileH);
+    const auto   loadTile = [&](uint32_t tt, f16x8(&A)[KS]) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            A[s] = th[(static_cast<size_t>(tt) * KS + s) * 64 + lane];
+    };
+    const f16x8* fh = static_cast<const f16x8*>(a.frameH);
+    f16x8        B[NB][KS];
+    float        kap[NB];  // 0.5 log2(e) 2^e of this lane's frame in block b
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            B[b][s] = fh[(static_cast<size_t>(fb0 + b) * KS + s) * 64 + lane];
+        kap[b] = ldexpf(0.721347520f, a.frameExp[frame0 + 32u * b + (static_cast<uint32_t>(lane) & 31u)]);
+    }
+    // frame operands complete before the tile prefetch, then pinned to the accumulator file
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            asm volatile("" : "+a"(B[b][s]));
+        asm volatile("" ::"v"(kap[b]));
+    }
+    f16x8 R0[KS], R1[KS];  // tiles t (even steps) and t + 1; the padded tile array keeps loads past T1 in bounds
+    loadTile(T0, R0);
+    loadTile(T0 + 1, R1);
+
+    const uint32_t kmask = BEST ? (1u << a.tileBits) - 1u : 0u;  // scores only: untagged values
+    uint32_t       vmask = ~kmask;
+    asm volatile("" : "+v"(vmask));
+
+    uint32_t   best[NB][2];  // slot 0: registers 0..7, slot 1: 8..15 (the key carries the register)
+    float      S[NB][2], Rf[NB];
+    const auto resetBest = [&]() {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            Rf[b]      = 1e30f;  // no reference yet: the first tile sets it (S = 0 * 2^-huge = 0)
+            best[b][0] = best[b][1] = 0xffffffffu;
+            S[b][0] = S[b][1] = 0.0f;
+        }
+    };
+    const auto chain = [&](const f16x8(&A)[KS], f32x16(&acc)[NB]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            acc[b] = f32x16{};  // ||x'||^2 is in K: the chain starts from an inline 0
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[b][s], acc[b], 0, 0, 0);
+    };
+    const auto epilogue = [&](const f32x16(&acc)[NB], uint32_t tl) __attribute__((always_inline)) {
+        uint32_t tag[16];  // opaque SGPRs (one v_and_or_b32 per key)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            tag[i] = (tl << 4) | static_cast<uint32_t>(i);
+            asm("" : "+s"(tag[i]));
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            uint32_t k[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                k[i] = BEST ? (__float_as_uint(acc[b][i]) & vmask) | tag[i] : __float_as_uint(acc[b][i]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                best[b][h] = umin3(umin3(umin3(umin3(best[b][h], k[8 * h], k[8 * h + 1]), k[8 * h + 2], k[8 * h + 3]),
+                                         k[8 * h + 4], k[8 * h + 5]),
+                                   k[8 * h + 6], k[8 * h + 7]);
+            // online rescale to the running minimum: every exponent below stays <= 0
+            const float vmin = __uint_as_float(min(best[b][0], best[b][1]) & vmask);
+            const float nr   = fminf(Rf[b], kap[b] * vmin);
+            const float f    = __builtin_amdgcn_exp2f(nr - Rf[b]);
+            Rf[b]            = nr;
+            S[b][0] *= f;
+            S[b][1] *= f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                S[b][i & 1] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[b][i], -kap[b], nr));
+        }
+    };
+
+    uint32_t m = m0, tBeg = T0, tEnd = m0 < m1 ? mixTileOff[m0 + 1] : T0;
+    resetBest();
+    const auto emit = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            emitMixtureSplit32Sum<BEST>(a, *reinterpret_cast<const uint32_t(*)[2][2]>(&best[2 * h]),
+                                        *reinterpret_cast<const float(*)[2][2]>(&S[2 * h]),
+                                        *reinterpret_cast<const float(*)[2]>(&Rf[2 * h]), m, frame0 + 64u * h, lane,
+                                        kmask);
+    };
+    const auto advance = [&](uint32_t tNext) __attribute__((always_inline)) {
+        ++m;
+        tBeg = tNext;
+        tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        while (m < m1 && tEnd == tNext) {
+            emit();
+            ++m;
+            tEnd = m < m1 ? mixTileOff[m + 1] : tNext;
+        }
+    };
+    const auto finish = [&](uint32_t tNext) __attribute__((always_inline)) {
+        if (tNext == tEnd) {
+            emit();
+            resetBest();
+            advance(tNext);
+        }
+    };
+    // MFMAs of the tile in A into cur beside the epilogue of tile tPrev (in prev)
+    const auto step = [&](const f16x8(&A)[KS], f32x16(&cur)[NB], const f32x16(&prev)[NB], uint32_t tPrev)
+            __attribute__((always_inline)) {
+        chain(A, cur);
+        epilogue(prev, tPrev - tBeg);
+#pragma unroll
+        for (int i = 0; i < NB * KS; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, GMM_SPLIT32_SUM_IL, 0);  // VALU
+        }
+    };
+
+    while (m < m1 && tEnd == T0) {  // mixtures without tiles at the start of the chunk
+        emit();
+        ++m;
+        tEnd = m < m1 ? mixTileOff[m + 1] : T0;
+    }
+    if (T0 < T1) {
+        f32x16   accX[NB], accY[NB];
+        uint32_t t = T0;
+        chain(R0, accX);  // tile T0: nothing to finish beside it
+        loadTile(t + 2, R0);
+        t += 1;
+        for (; t + 2 <= T1; t += 2) {
+            step(R1, accY, accX, t - 1);
+            loadTile(t + 2, R1);
+            finish(t);
+            step(R0, accX, accY, t);
+            loadTile(t + 3, R0);
+            finish(t + 1);
+        }
+        if (t < T1) {  // one more tile (in R1)
+            step(R1, accY, accX, t - 1);
+            finish(t);
+            epilogue(accY, t - tBeg);
+            finish(t + 1);
+        }
+        else {
+            epilogue(accX, t - 1 - tBeg);
+            finish(t);
+        }
+    }
+}
+
 }  // namespace dev
 
 hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
@@ -1390,10 +1622,36 @@ static void launchSplitSumK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
                            0, s, a, a.mixTileOff);
 }
 
-hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t kSteps16, hipStream_t stream) {
+template <int KS>
+static void launchSplit32SumK(const SplitArgs& a, uint32_t grid, hipStream_t s) {
+    if (a.best)
+        hipLaunchKernelGGL((dev::scoreSplit32Sum<KS, true>), dim3(grid), dim3(64 * (kSplitFramesPerBlock / 128)), 0, s, a,
+                           a.mixTileOff);
+    else
+        hipLaunchKernelGGL((dev::scoreSplit32Sum<KS, false>), dim3(grid), dim3(64 * (kSplitFramesPerBlock / 128)), 0, s,
+                           a, a.mixTileOff);
+}
+
+hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t rows, uint32_t kSteps16, hipStream_t stream) {
     const uint32_t grid = 8u * ((a.nChunks + 7u) / 8u) * a.nFrameTiles;
     if (grid == 0)
         return hipSuccess;
+    if (rows == 32) {
+        switch (kSteps16) {
+            case 1: launchSplit32SumK<1>(a, grid, stream); break;
+            case 2: launchSplit32SumK<2>(a, grid, stream); break;
+            case 3: launchSplit32SumK<3>(a, grid, stream); break;
+            case 4: launchSplit32SumK<4>(a, grid, stream); break;
+            case 5: launchSplit32SumK<5>(a, grid, stream); break;
+            case 6: launchSplit32SumK<6>(a, grid, stream); break;
+            case 7: launchSplit32SumK<7>(a, grid, stream); break;
+            case 8: launchSplit32SumK<8>(a, grid, stream); break;
+            case 9: launchSplit32SumK<9>(a, grid, stream); break;
+            case 10: launchSplit32SumK<10>(a, grid, stream); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (kSteps16) {
         case 1: launchSplitSumK<1>(a, grid, stream); break;
         case 2: launchSplitSumK<2>(a, grid, stream); break;

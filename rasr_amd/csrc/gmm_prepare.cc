@@ -676,9 +676,10 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
     // K column, profiles/r05/s20)
     const bool     saves32   = splitKSteps32(D) * 16 * 105 < splitKSteps(D) * 32 * 100;
     const bool     want32    = splitRowsWanted == 32 || (splitRowsWanted == 0 && saves32);
-    // diagonal-sum: 16-row tiles only (scoreSplitSum)
-    const uint32_t rows      = (flavor != Flavor::DiagonalSum && fits32 && (want32 || keyBits16 > 8))
-                                   ? 32 : (keyBits16 <= 8 ? 16 : 0);
+    // diagonal-sum: 32-row tiles wherever they fit (scoreSplit32Sum: its VALU-bound epilogue gets 1.5x the issue
+    // cycles per unit of matrix work on the 32x32x16 shape), unless 16 rows are asked for (scoreSplitSum)
+    const bool     sum32     = flavor == Flavor::DiagonalSum && splitRowsWanted != 16;
+    const uint32_t rows      = (fits32 && (want32 || sum32 || keyBits16 > 8)) ? 32 : (keyBits16 <= 8 ? 16 : 0);
     if (wantSplit && !out.foldNorm && splitKSteps(D) <= 8 && T > 0 && rows != 0) {
         std::vector<double> maxAbs(D, 0.0);
         double              maxConst = 0;

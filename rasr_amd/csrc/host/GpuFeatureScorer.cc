@@ -244,6 +244,9 @@ public:
     // the position's best-density row once its call carried one (the same generation check as score(e)); a
     // position of a score-only call answers through getBestDensity (one pair, or the call's whole table)
     DensityInMixture bestDensity(EmissionIndex e) const override {
+        DensityInMixture v;
+        if (parent_->sparseAnswer(currentFeature_, e, &v))  // answered alone before: that answer (memoized)
+            return v;
         const uint32_t g = parent_->positionGeneration(currentFeature_);
         if (!bestRow_ || g != bestGen_) {
             bestRow_ = parent_->bestRow(currentFeature_, buffered_);
@@ -401,6 +404,7 @@ void GpuBatchFeatureScorer::reset() const {
     std::fill(cached_.begin(), cached_.end(), 0);
     for (uint32_t& g : generation_)
         ++g;
+    sparse_.clear();  // every position's frame is gone
     pendingCount_   = 0;
     currentFeature_ = 0;
     buffered_       = 0;
@@ -412,6 +416,10 @@ void GpuBatchFeatureScorer::setFeature(size_t pos, const FeatureVector& f) const
         landInflight();
     std::copy(f.begin(), f.end(), features_.data() + pos * dimension_);
     ++generation_[pos];
+    // the position's single-pair answers belonged to its previous frame (once every position took a new frame
+    // the map is empty and bestDensity() skips the lookup)
+    for (auto i = sparse_.begin(); i != sparse_.end();)
+        i = (i->first >> 32) == pos ? sparse_.erase(i) : std::next(i);
     if (!prefetchChunk_)
         return;
     // the new frame joins the pending run (it is the newest buffered position)
@@ -545,6 +553,17 @@ const DensityInMixture* GpuBatchFeatureScorer::bestRow(uint32_t featureIndex, ui
     return bestCached_[p] ? best_.data() + static_cast<size_t>(p) * rowStride() : nullptr;
 }
 
+bool GpuBatchFeatureScorer::sparseAnswer(uint32_t featureIndex, EmissionIndex e, DensityInMixture* v) const {
+    if (sparse_.empty())
+        return false;
+    const uint32_t p  = featureIndex % bufferSize_;
+    const auto     it = sparse_.find((static_cast<uint64_t>(p) << 32) | e);
+    if (it == sparse_.end() || it->second.first != generation_[p])
+        return false;
+    *v = it->second.second;
+    return true;
+}
+
 DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const {
     assert(e < nMixtures_);
     if (!assigning_)
@@ -557,10 +576,10 @@ DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t
         fill(featureIndex, length, true);
     const size_t o = static_cast<size_t>(p) * rowStride() + e;
     // a pair answered alone for this frame keeps its answer (memoized as the reference's context scorer does)
-    const uint64_t key = (static_cast<uint64_t>(p) << 32) | e;
-    const auto     it  = sparse_.find(key);
-    if (it != sparse_.end() && it->second.first == generation_[p])
-        return it->second.second;
+    const uint64_t   key = (static_cast<uint64_t>(p) << 32) | e;
+    DensityInMixture memo;
+    if (sparseAnswer(featureIndex, e, &memo))
+        return memo;
     if (bestCached_[p])
         return best_[o];
     // a position of a score-only call (made before the first bestDensity()): the asked pair alone while that

@@ -241,6 +241,8 @@ public:
     uint32_t         positionGeneration(uint32_t featureIndex) const { return generation_[featureIndex % bufferSize_]; }
     // 0xffffffff for the batch types, which have no assignment (as ContextScorer::bestDensity)
     DensityInMixture getBestDensity(EmissionIndex e, uint32_t featureIndex, uint32_t length) const;
+    // the single-pair answer of (position, e) for the position's current frame, if one was given
+    bool             sparseAnswer(uint32_t featureIndex, EmissionIndex e, DensityInMixture* v) const;
     // the best densities of every emission of the position (filled first if needed, with best densities), or NULL
     // while they are not in the table (a score-only call's position: getBestDensity answers); valid as scoreRow()
     const DensityInMixture* bestRow(uint32_t featureIndex, uint32_t length) const;

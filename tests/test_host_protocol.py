@@ -351,6 +351,7 @@ def test_best_density_memoized_across_table_switch(gpu, tmp_path, kind, buffer_s
     is the reference's."""
     ms = ra.synthetic_mixture_set(40, 4, 39, seed=69, weights="random")
     ms.means[1] = ms.means[0]
+    ms.means[2:4] = ms.means[0] + 30.0  # never the best: the tie is between densities 0 and 1 in every frame
     lw = np.log(0.25)
     ms.mixture_log_weights[:4] = [lw, lw + 5e-5, np.log(0.3), np.log(0.2) - 1e-2]
     frames = ra.synthetic_frames(24, 39, seed=70)
