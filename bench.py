@@ -106,6 +106,8 @@ def parse():
     p.add_argument("--dim", type=int, default=39)
     p.add_argument("--ragged", action="store_true",
                    help="SURVEY 8(d) ragged variant: K_m ~ U[64, 256] with the same total of densities")
+    p.add_argument("--tying", choices=["pooled", "mixture-specific", "none"], default="pooled",
+                   help="covariance tying of the synthetic model (RASR covariance-tying; the configs are pooled)")
     p.add_argument("--no-best", action="store_true", help="do not write best-density indices")
     p.add_argument("--no-extra-mode", action="store_true", help="do not time the other mode")
     p.add_argument("--nn-activation", default="sigmoid", choices=["sigmoid", "tanh", "relu", "elu", "identity"],
@@ -329,7 +331,8 @@ def run_mode(args, mode, ms, ws, rank, local, launches):
         issued = 2.0 * 64 * ((args.dim + 63) // 64) * d_local * fpl
     sec = kms_avg * 1e-3
     achieved = algo / sec / 1e12
-    default_model = args.dim == 39 and not args.ragged and args.mixtures == 5000 and args.densities == 160
+    default_model = (args.dim == 39 and not args.ragged and args.mixtures == 5000 and args.densities == 160
+                     and args.tying == "pooled")
     traffic, traffic_src = load_pmc(mode, fpl, default_model) if not sharded else (None, None)
     res = {
         "value": total_frames / dt_max,
@@ -982,6 +985,7 @@ def make_line(args, res, ws: int) -> dict:
             "scorer": MODES[args.mode][0],
             "mixtures": args.mixtures,
             "densities_per_mixture": "U[64, 256] (ragged, same total)" if args.ragged else args.densities,
+            "covariance_tying": args.tying,
             "dimension": args.dim,
             "frames_per_gpu_per_step": res["frames_per_step"],
             "frames_per_launch": res["frames_per_launch"],
@@ -1061,7 +1065,8 @@ def main():
     else:
         import rasr_amd as ra
         counts = (ra.ragged_counts(args.mixtures, args.mixtures * args.densities) if args.ragged else args.densities)
-        ms = ra.synthetic_mixture_set(args.mixtures, counts, args.dim, seed=2024)
+        ms = ra.synthetic_mixture_set(args.mixtures, counts, args.dim, seed=2024,
+                                      tying=None if args.tying == "pooled" else args.tying)
         res = run_mode(args, args.mode, ms, ws, rank, local, launches)
     guard.headline_done = True
     if rank == 0:

@@ -146,6 +146,7 @@ struct gmm_scorer {
     uint32_t          directL    = 0;      // row length of the direct layout
     uint32_t          kSteps16   = 0;      // split kernel: K steps (32 wide for 16-row tiles, 16 wide for 32-row)
     uint32_t          splitRows  = 16;     // split kernel tile height
+    bool              splitCov   = false;  // split kernels, several covariances (covariance-free frame operand)
     uint32_t          tileBits   = 1;
     float             offsetK0   = 0;
     // density preselection (preselection-batch-*)
@@ -520,9 +521,13 @@ int scoreImpl(gmm_scorer* s, const float* frames, uint32_t nFrames, uint32_t fra
         GMM_HIP_CHECK(span.end());
     }
     else if (s->split) {
-        GMM_HIP_CHECK(launchPrepareFramesSplit(frames, nFrames, frameStride, nPadCall, s->D, s->splitRows, s->kSteps16, s->dIsv,
-                                               s->dCentre, s->dDimScale, s->dLimbExp, s->dFrameH, s->dFrameXX, s->dFrameExp,
-                                               stream));
+        if (s->splitCov)
+            GMM_HIP_CHECK(launchPrepareFramesSplitCov(frames, nFrames, frameStride, nPadCall, s->D, s->kSteps16, s->dCentre,
+                                                      s->dDimScale, s->dLimbExp, s->dFrameH, s->dFrameExp, stream));
+        else
+            GMM_HIP_CHECK(launchPrepareFramesSplit(frames, nFrames, frameStride, nPadCall, s->D, s->splitRows, s->kSteps16,
+                                                   s->dIsv, s->dCentre, s->dDimScale, s->dLimbExp, s->dFrameH, s->dFrameXX,
+                                                   s->dFrameExp, stream));
         SplitArgs a{};
         a.tileH       = s->dTileA;
         a.mixTileOff  = s->dMixTileOff;
@@ -624,6 +629,26 @@ void gmm_default_config(gmm_scorer_config* cfg) {
 }  // extern "C"
 
 namespace {
+
+// The quantized scorer with several covariances (and the native f32 kernel) prepares the frames once per
+// covariance, as the reference's Context does (SimdFeatureScorer.cc:22-35): a C x frames table.  A table past three
+// quarters of the device's free memory is refused with its size (an untied 800k model at 32768 frames would need
+// terabytes); the float types on the covariance-free split layout need no such table.
+int checkCovarianceTable(size_t bytes, uint32_t C, uint32_t maxFrames) {
+    if (C <= 1)
+        return GMM_OK;
+    size_t freeB = 0, totalB = 0;
+    if (hipMemGetInfo(&freeB, &totalB) != hipSuccess)
+        freeB = 0;
+    if (bytes <= freeB / 4 * 3)
+        return GMM_OK;
+    char msg[320];
+    std::snprintf(msg, sizeof(msg),
+                  "%u covariances x %u frames need %.1f GiB of per-covariance frame operands (%.1f GiB free): lower "
+                  "max_frames / buffer-size, or use a float scorer type (covariance-free layout, no such table)",
+                  C, maxFrames, static_cast<double>(bytes) / (1u << 30), static_cast<double>(freeB) / (1u << 30));
+    return fail(GMM_ERR_UNSUPPORTED, msg);
+}
 
 // preselection: the clustering over all entries' prepared means, the tiles' row cluster offsets and the
 // per-call mask table.  rowEntry / fill: the scorer tiling (16 rows) and, for the split layout, the
@@ -1413,6 +1438,8 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
             (rc = upload(&s->dIsv, p.isvDevice)))
             return rc;
         const size_t nQ = static_cast<size_t>(s->C) * s->nFramesPad;
+        if ((rc = checkCovarianceTable(nQ * (s->kSteps * kI8K + sizeof(int32_t)), s->C, cfg.max_frames)) != GMM_OK)
+            return rc;
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameQ), nQ * s->kSteps * kI8K));
         GMM_HIP_CHECK(hipMemset(s->dFrameQ, 0, nQ * s->kSteps * kI8K));
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameSS), nQ * sizeof(int32_t)));
@@ -1455,6 +1482,7 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
             return fail(GMM_ERR_UNSUPPORTED, "preselection-batch-float needs the 16-row split-f16 layout (one "
                                              "covariance, dimension <= 83, <= 1024 densities per mixture)");
         s->split    = p.split;
+        s->splitCov = p.splitCov;
         s->kSteps16 = p.kSteps16;
         s->splitRows = p.splitRows;
         // wide workgroups of 192 frames (K steps 5) read up to 191 rows past the call: room for them in the frame
@@ -1512,6 +1540,8 @@ int createScorer(const gmm_mixture_set* ms, gmm_scorer_type type, const gmm_scor
             (rc = upload(&s->dCentre, p.centre)))
             return rc;
         const size_t nX = static_cast<size_t>(s->C) * s->nFramesPad;
+        if ((rc = checkCovarianceTable(nX * (s->kSteps * 4 + 1) * sizeof(float), s->C, cfg.max_frames)) != GMM_OK)
+            return rc;
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameX), nX * s->kSteps * 4 * sizeof(float)));
         GMM_HIP_CHECK(hipMemset(s->dFrameX, 0, nX * s->kSteps * 4 * sizeof(float)));
         GMM_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s->dFrameXX), nX * sizeof(float)));
@@ -1703,11 +1733,13 @@ int gmm_scorer_create_sharded(const gmm_mixture_set* ms, gmm_scorer_type type, c
     s->flavor     = m ? m->flavor : Flavor::Simd;
     s->quantized  = m ? m->quantized : false;
     s->split      = m ? m->split : false;
+    s->splitCov   = m ? m->splitCov : false;
     s->direct     = m ? m->direct : false;
     s->splitRows  = m ? m->splitRows : 16;
     s->kSteps16   = m ? m->kSteps16 : 0;
     s->device     = g->lead;
     s->cfg        = cfg;
+    s->cfg.cache_archive = nullptr;  // valid only during create (the parts took their copies)
     s->D          = ms->dimension;
     s->C          = ms->n_covariances;
     s->nMix       = ms->n_mixtures;

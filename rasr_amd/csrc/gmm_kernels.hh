@@ -140,6 +140,10 @@ inline uint32_t splitKSteps(uint32_t dimension) {  // K/32 steps of v_mfma_f32_1
 inline uint32_t splitKSteps32(uint32_t dimension) {  // K/16 steps of v_mfma_f32_32x32x16_f16
     return (3 * dimension + kSplitLimbs + kSplitXXLimbs + 15) / 16;
 }
+// several covariances (the covariance-free layout): K = [y^2 terms 3D][y terms 3D][row-constant limbs 4]
+inline uint32_t splitCovKSteps(uint32_t dimension) {
+    return (6 * dimension + kSplitLimbs + 31) / 32;
+}
 
 struct SplitArgs {
     const void*     tileH;        // f16 [T+pad][KS16][64][8]
@@ -176,6 +180,10 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
                                     const float* dimScale,
                                     const int32_t* limbExp, void* frameH, float* frameXX, int32_t* frameExp,
                                     hipStream_t stream);
+// several covariances: frameH [nFramesPad/16][KS16][64][8] with the K layout of splitCovKSteps, frameExp = e
+hipError_t launchPrepareFramesSplitCov(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
+                                       uint32_t D, uint32_t kSteps, const float* centre, const float* dimScale,
+                                       const int32_t* limbExp, void* frameH, int32_t* frameExp, hipStream_t stream);
 hipError_t launchScoreSplit(const SplitArgs& a, uint32_t rows, uint32_t kSteps, hipStream_t stream);
 hipError_t launchScoreSplitSum(const SplitArgs& a, uint32_t rows, uint32_t kSteps, hipStream_t stream);  // diagonal-sum
 constexpr uint32_t kSplit32MaxKSteps = 10;  // 32-row split kernel instantiated for K/16 <= 10 (D <= 51)

@@ -204,6 +204,79 @@ __global__ __launch_bounds__(256) void prepareFramesSplit(const float* __restric
 }
 
 // ---------------------------------------------------------------------------
+// frame preparation for several covariances (the covariance-free layout, gmm_prepare.cc): y = x - c in f32,
+// Y = y^2 2^a_d and z = y 2^b_d (dimScale [0, D) and [D, 2D)), the frame exponent e keeping max(|Y|, |z|) 2^-e
+// below 2^15, K = [Yh, Yl, Yh][zh, zl, zh][2^(b_s - e) limbs].  32 threads per frame, 8 frames per block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prepareFramesSplitCov(const float* __restrict__ frames, uint32_t nFrames,
+                                                              uint32_t frameStride, uint32_t nFramesRead, uint32_t D,
+                                                              uint32_t KS16, const float* __restrict__ centre,
+                                                              const float* __restrict__ dimScale,
+                                                              const int32_t* __restrict__ limbExp,
+                                                              u32x4* __restrict__ frameH, int32_t* __restrict__ frameExp) {
+    __shared__ float ys[8][128];  // y of the block's frames (D <= 126)
+    __shared__ int   shE[8];
+    const uint32_t   fl = threadIdx.x >> 5, t = threadIdx.x & 31u;
+    const uint32_t   f       = blockIdx.x * 8u + fl;
+    const bool       inRange = f < nFramesRead, valid = f < nFrames;
+    const float*     x       = frames + static_cast<size_t>(f) * frameStride;
+    float            ymax    = 0.0f;
+    int              finite  = 1;
+    if (valid)
+        for (uint32_t k = t; k < D; k += 32u) {
+            const float y = __fsub_rn(x[k], centre[k]);
+            ys[fl][k]     = y;
+            const float a = fabsf(__fmul_rn(__fmul_rn(y, y), dimScale[k]));
+            const float b = fabsf(__fmul_rn(y, dimScale[D + k]));
+            finite        = finite && a <= 3.40282347e+38f && b <= 3.40282347e+38f;
+            ymax          = fmaxf(ymax, fmaxf(a, b));
+        }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        ymax   = fmaxf(ymax, __shfl_xor(ymax, o, 32));
+        finite = finite & __shfl_xor(finite, o, 32);
+    }
+    if (t == 0 && inRange) {
+        int e = 0;
+        if (valid && finite && ymax > 32768.0f) {
+            int ex;
+            frexpf(ymax, &ex);  // ymax in [2^(ex-1), 2^ex)
+            e = ex - 15;
+        }
+        frameExp[f] = e;
+        shE[fl]     = e;
+    }
+    __syncthreads();
+    if (!inRange)
+        return;
+    const int e = shE[fl];
+    // B fragments (16-row tiles): frame block f/16, lane 16*((k>>3)&3) + f%16, step k>>5
+    const uint32_t fb = f / 16u, col = f % 16u;
+    for (uint32_t q = t; q < KS16 * 4; q += 32u) {  // groups of 8 consecutive k
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (valid)
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t k = 8 * q + j;
+                uint16_t       h = 0;
+                if (k < 6 * D) {
+                    const uint32_t part = k / D, d = k - part * D;
+                    const float    y    = ys[fl][d];
+                    const float    v    = part < 3 ? ldexpf(__fmul_rn(__fmul_rn(y, y), dimScale[d]), -e)
+                                                   : ldexpf(__fmul_rn(y, dimScale[D + d]), -e);
+                    const uint16_t hi = h16bits(v);
+                    h = (part == 1 || part == 4) ? h16bits(v - static_cast<float>(__builtin_bit_cast(_Float16, hi))) : hi;
+                }
+                else if (k < 6 * D + kSplitLimbs) {
+                    const int be = limbExp[k - 6 * D] - e;
+                    h            = be < -24 ? 0 : h16bits(ldexpf(1.0f, be));
+                }
+                w[j >> 1] |= static_cast<uint32_t>(h) << (16 * (j & 1));
+            }
+        frameH[(static_cast<size_t>(fb) * KS16 + (q >> 2)) * 64 + 16 * (q & 3) + col] = u32x4{w[0], w[1], w[2], w[3]};
+    }
+}
+
+// ---------------------------------------------------------------------------
 // keys: a row's value v > 0 (row constants shifted by K0, ||x'||^2 the initial accumulator) is kept
 // as the u32 bits of the float with the low keyBits mantissa bits replaced by (tile << 2 | r), r the
 // accumulator slot (row 4g + r of the tile in lane group g).  Positive floats order like their bits,
@@ -587,6 +660,9 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
 #ifndef GMM_SPLIT_WIDE_IL
 #define GMM_SPLIT_WIDE_IL 48  // MFMAs of a step interleaved 1 : 2 with the epilogue's VALU (at 16 blocks)
 #endif
+#ifndef GMM_SPLIT_WIDE_SLOTS
+#define GMM_SPLIT_WIDE_SLOTS 2  // running minima per column block (1: the two min3 of a block chained)
+#endif
 
 template <int KS, bool BEST>
 __global__ __launch_bounds__(64, 1) void scoreSplitWide(SplitArgs a, const uint32_t* __restrict__ mixTileOff) {
@@ -639,7 +715,8 @@ __global__ __launch_bounds__(64, 1) void scoreSplitWide(SplitArgs a, const uint3
     asm volatile("" : "+v"(vmask));
     const float noneScore = __fmul_rn(a.outScale, a.flavor == 2 ? 0.5f * 3.40282347e+38f : 3.40282347e+38f);
 
-    uint32_t   best[NF][2];  // slot 0: rows 4g, 4g + 1; slot 1: rows 4g + 2, 4g + 3
+    // slot 0: rows 4g, 4g + 1; slot 1: rows 4g + 2, 4g + 3 (GMM_SPLIT_WIDE_SLOTS 1: one slot, the min3 chained)
+    uint32_t   best[NF][2];
     const auto resetBest = [&]() {
 #pragma unroll
         for (int cb = 0; cb < NF; ++cb)
@@ -668,8 +745,12 @@ __global__ __launch_bounds__(64, 1) void scoreSplitWide(SplitArgs a, const uint3
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 v[r] = BEST ? (__float_as_uint(acc[cb][r]) & vmask) | tag[r] : __float_as_uint(acc[cb][r]);
+#if GMM_SPLIT_WIDE_SLOTS == 1
+            best[cb][0] = umin3(umin3(best[cb][0], v[0], v[1]), v[2], v[3]);
+#else
             best[cb][0] = umin3(best[cb][0], v[0], v[1]);
             best[cb][1] = umin3(best[cb][1], v[2], v[3]);
+#endif
         }
     };
 
@@ -1536,6 +1617,15 @@ hipError_t launchPrepareFramesSplit(const float* frames, uint32_t nFrames, uint3
         hipLaunchKernelGGL(dev::prepareFramesSplit<16>, dim3((nFramesRead + 7) / 8), dim3(256), 0, stream, frames,
                            nFrames, frameStride, nFramesRead, D, kSteps, isv, centre, dimScale, limbExp,
                            static_cast<dev::u32x4*>(frameH), frameXX, frameExp);
+    return hipGetLastError();
+}
+
+hipError_t launchPrepareFramesSplitCov(const float* frames, uint32_t nFrames, uint32_t frameStride, uint32_t nFramesRead,
+                                       uint32_t D, uint32_t kSteps, const float* centre, const float* dimScale,
+                                       const int32_t* limbExp, void* frameH, int32_t* frameExp, hipStream_t stream) {
+    hipLaunchKernelGGL(dev::prepareFramesSplitCov, dim3((nFramesRead + 7) / 8), dim3(256), 0, stream, frames, nFrames,
+                       frameStride, nFramesRead, D, kSteps, centre, dimScale, limbExp, static_cast<dev::u32x4*>(frameH),
+                       frameExp);
     return hipGetLastError();
 }
 

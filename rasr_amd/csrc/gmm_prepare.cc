@@ -118,7 +118,8 @@ std::string validate(const gmm_mixture_set& ms) {
     return "";
 }
 
-static void buildTiling(const gmm_mixture_set& ms, ShardRange shard, Tiling& t, uint32_t rows = kTileRows) {
+static void buildTiling(const gmm_mixture_set& ms, ShardRange shard, Tiling& t, uint32_t rows = kTileRows,
+                        bool groupByCovariance = true) {
     const uint32_t nMix = shard.end - shard.begin;
     t.mixTileOffset.assign(nMix + 1, 0);
     t.tileCovariance.clear();
@@ -133,15 +134,17 @@ static void buildTiling(const gmm_mixture_set& ms, ShardRange shard, Tiling& t, 
         t.maxEntriesPerMixture = std::max(t.maxEntriesPerMixture, e - b);
         order.resize(e - b);
         std::iota(order.begin(), order.end(), b);
-        // group rows by covariance (one frame-side operand per tile); stable keeps entry order
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-            return ms.density_covariance[ms.mixture_densities[x]] < ms.density_covariance[ms.mixture_densities[y]];
-        });
+        // group rows by covariance (one frame-side operand per tile); stable keeps entry order.  Without grouping
+        // (the covariance-free split layout) a tile takes 16 consecutive entries whatever their covariances
+        if (groupByCovariance)
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+                return ms.density_covariance[ms.mixture_densities[x]] < ms.density_covariance[ms.mixture_densities[y]];
+            });
         size_t i = 0;
         while (i < order.size()) {
             const uint32_t cov = ms.density_covariance[ms.mixture_densities[order[i]]];
             size_t         j   = i;
-            while (j < order.size() && ms.density_covariance[ms.mixture_densities[order[j]]] == cov)
+            while (j < order.size() && (!groupByCovariance || ms.density_covariance[ms.mixture_densities[order[j]]] == cov))
                 ++j;
             for (size_t r0 = i; r0 < j; r0 += rows) {
                 t.tileCovariance.push_back(cov);
@@ -813,8 +816,162 @@ std::string prepareFloat(const gmm_mixture_set& ms, Flavor flavor, float mixture
         }
     }
 
+    // ---- split-f16 layout for several covariances (round 6): the covariance-free expansion ----
+    // With y = x - c (the frame about the centre), mu' = mu - c and w = isv^2 of the row's covariance,
+    //     ||(x - mu) isv||^2 = sum_d w_d y_d^2 - 2 sum_d w_d mu'_d y_d + sum_d w_d mu'_d^2,
+    // so one frame operand [y^2, y] serves every covariance (no C x frames buffers, no tiles split by covariance):
+    // K = [0,D) wh Yh, [D,2D) wh Yl, [2D,3D) wl Yh, [3D,4D) nh zh, [4D,5D) nh zl, [5D,6D) nl zh, [6D,6D+4) the row
+    // constant's limbs, where Y = y^2 2^a_d, z = y 2^b_d (frame side), w'' = w 2^-a_d, n'' = -2 w mu' 2^-b_d (model
+    // side), the powers of two putting the model's largest |w''| and |n''| of a dimension in [2^7, 2^8).  Twice
+    // the pooled layout's K (6 D + 4: 238 -> 256 at D = 39), on the same kernels (they are K-agnostic), against the
+    // native f32 kernel's 1/16-rate MFMAs and per-covariance frame operands.
+    const uint32_t keyBitsCov = bitsFor(((maxEntries + 15) / 16 + 1) & ~1u) + 2;
+    if (wantSplit && out.foldNorm && splitCovKSteps(D) <= 8 && T > 0 && keyBitsCov <= 8) {
+        Tiling st;
+        buildTiling(ms, shard, st, 16, false);
+        double minC = 1.0;
+        for (uint32_t e : st.rowEntry)
+            if (e != UINT32_MAX)
+                minC = std::min(minC, rowConstant(e));
+        const float k0 = minC < 1.0 ? static_cast<float>(std::ceil(1.0 - minC)) : 0.0f;
+        // per row: w_d, n_d = -2 w_d mu'_d (f64) and the constant sum w mu'^2 + c_row + K0
+        const auto covValues = [&](uint32_t e, double* w, double* n, double& c) -> bool {
+            if (e == UINT32_MAX)
+                return false;
+            const uint32_t dns  = ms.mixture_densities[e];
+            const uint32_t cov  = ms.density_covariance[dns];
+            const float*   mean = ms.means + static_cast<size_t>(ms.density_mean[dns]) * D;
+            const float*   iv   = out.isv.data() + static_cast<size_t>(cov) * D;
+            double         mm   = 0;
+            for (uint32_t k = 0; k < D; ++k) {
+                const double wk = static_cast<double>(iv[k]) * iv[k];
+                const double mp = static_cast<double>(mean[k]) - out.centre[k];
+                w[k]            = wk;
+                n[k]            = -2.0 * wk * mp;
+                mm += wk * mp * mp;
+            }
+            c = mm + rowConstant(e) + k0;
+            return true;
+        };
+        std::vector<double> wv(D), nv(D), maxW(D, 0.0), maxN(D, 0.0);
+        double              cv = 0, maxConst = 0;
+        for (uint32_t e : st.rowEntry)
+            if (covValues(e, wv.data(), nv.data(), cv)) {
+                for (uint32_t k = 0; k < D; ++k) {
+                    maxW[k] = std::max(maxW[k], std::fabs(wv[k]));
+                    maxN[k] = std::max(maxN[k], std::fabs(nv[k]));
+                }
+                maxConst = std::max(maxConst, std::fabs(cv));
+            }
+        const double padBias = flavor == Flavor::DiagonalSum ? std::ldexp(1.0, 29) : 0.0;
+        maxConst += padBias;
+        bool finite = std::isfinite(maxConst);
+        for (uint32_t k = 0; k < D; ++k)
+            finite = finite && std::isfinite(maxW[k]) && std::isfinite(maxN[k]);
+        int b0 = 9;
+        while (b0 < 15 && maxConst / std::ldexp(1.0, b0) > 32768.0)
+            ++b0;
+        if (finite && maxConst / std::ldexp(1.0, b0) <= 32768.0) {
+            out.split        = true;
+            out.splitCov     = true;
+            out.splitRows    = 16;
+            out.kSteps16     = splitCovKSteps(D);
+            out.splitKeyBits = keyBitsCov;
+            out.offsetK0     = k0;
+            // an even tile count per mixture (the pair kernel), the pad tile repeating the mixture's first row
+            std::vector<uint32_t> fillEntry;
+            Tiling                pt;
+            pt.rows                 = 16;
+            pt.maxEntriesPerMixture = st.maxEntriesPerMixture;
+            pt.mixTileOffset.assign(out.nMixtures + 1, 0);
+            for (uint32_t m = 0; m < out.nMixtures; ++m) {
+                const uint32_t b = st.mixTileOffset[m], e = st.mixTileOffset[m + 1];
+                for (uint32_t t = b; t < e; ++t) {
+                    pt.tileCovariance.push_back(st.tileCovariance[t]);
+                    fillEntry.push_back(st.rowEntry[static_cast<size_t>(t) * 16]);
+                    pt.rowEntry.insert(pt.rowEntry.end(), st.rowEntry.begin() + static_cast<size_t>(t) * 16,
+                                       st.rowEntry.begin() + static_cast<size_t>(t + 1) * 16);
+                    pt.rowDensityInMixture.insert(pt.rowDensityInMixture.end(),
+                                                  st.rowDensityInMixture.begin() + static_cast<size_t>(t) * 16,
+                                                  st.rowDensityInMixture.begin() + static_cast<size_t>(t + 1) * 16);
+                }
+                if ((e - b) & 1u) {
+                    pt.tileCovariance.push_back(st.tileCovariance[b]);
+                    fillEntry.push_back(st.rowEntry[static_cast<size_t>(b) * 16]);
+                    pt.rowEntry.insert(pt.rowEntry.end(), 16, UINT32_MAX);
+                    pt.rowDensityInMixture.insert(pt.rowDensityInMixture.end(), 16, UINT32_MAX);
+                }
+                pt.mixTileOffset[m + 1] = static_cast<uint32_t>(pt.tileCovariance.size());
+            }
+            pt.nTiles          = static_cast<uint32_t>(pt.tileCovariance.size());
+            out.tiling         = std::move(pt);
+            out.splitFillEntry = fillEntry;
+            for (uint32_t s2 = 0; s2 < kSplitLimbs; ++s2)
+                out.limbExp[s2] = b0 - 11 * static_cast<int32_t>(s2);
+            // frame-side multipliers: [0, D) 2^a_d for y^2, [D, 2D) 2^b_d for y
+            out.dimScale.assign(2 * D, 1.0f);
+            std::vector<double> inv(2 * D, 1.0);
+            for (uint32_t k = 0; k < 2 * D; ++k) {
+                const double mx = k < D ? maxW[k] : maxN[k - D];
+                if (mx > 0) {
+                    int ex;
+                    std::frexp(mx, &ex);
+                    const int a     = std::max(-60, std::min(60, ex - 1 - 7));
+                    out.dimScale[k] = static_cast<float>(std::ldexp(1.0, a));
+                    inv[k]          = std::ldexp(1.0, -a);
+                }
+            }
+            const auto h16 = [](double v) {
+                const _Float16 h = static_cast<_Float16>(v);
+                uint16_t       b;
+                std::memcpy(&b, &h, 2);
+                return b;
+            };
+            const auto f16v = [](uint16_t b) {
+                _Float16 h;
+                std::memcpy(&h, &b, 2);
+                return static_cast<double>(h);
+            };
+            const uint32_t TP = out.tiling.nTiles, KW = out.kSteps16 * 32;
+            out.tileH.assign(static_cast<size_t>(TP) * 16 * KW, 0);
+            std::vector<uint16_t> row(KW);
+            for (uint32_t t = 0; t < TP; ++t)
+                for (uint32_t r = 0; r < 16; ++r) {
+                    std::fill(row.begin(), row.end(), 0);
+                    const bool real = covValues(out.tiling.rowEntry[static_cast<size_t>(t) * 16 + r], wv.data(), nv.data(), cv);
+                    if (real || covValues(fillEntry[t], wv.data(), nv.data(), cv)) {
+                        if (!real)
+                            cv += padBias;
+                        for (uint32_t k = 0; k < D; ++k) {
+                            const float    w2 = static_cast<float>(wv[k] * inv[k]);
+                            const uint16_t wh = h16(w2);
+                            const uint16_t wl = h16(static_cast<double>(w2) - f16v(wh));
+                            row[k]            = wh;
+                            row[D + k]        = wh;
+                            row[2 * D + k]    = wl;
+                            const float    n2 = static_cast<float>(nv[k] * inv[D + k]);
+                            const uint16_t nh = h16(n2);
+                            const uint16_t nl = h16(static_cast<double>(n2) - f16v(nh));
+                            row[3 * D + k]    = nh;
+                            row[4 * D + k]    = nh;
+                            row[5 * D + k]    = nl;
+                        }
+                        double rem = cv;
+                        for (uint32_t s2 = 0; s2 < kSplitLimbs; ++s2) {
+                            const uint16_t l = h16(std::ldexp(rem, -out.limbExp[s2]));
+                            row[6 * D + s2]  = l;
+                            rem -= std::ldexp(f16v(l), out.limbExp[s2]);
+                        }
+                    }
+                    for (uint32_t k = 0; k < KW; ++k)  // v_mfma_f32_16x16x32_f16: lane 16((k>>3)&3) + row, step k>>5
+                        out.tileH[((static_cast<size_t>(t) * out.kSteps16 + (k >> 5)) * kLanes + 16 * ((k >> 3) & 3) + r) *
+                                          8 + (k & 7)] = row[k];
+                }
+        }
+    }
+
     if (flavor == Flavor::DiagonalSum && !out.split)
-        return "diagonal-sum runs on the split-f16 kernel only: one covariance, dimension <= 83, "
+        return "diagonal-sum runs on the split-f16 kernel only: dimension <= 83 (one covariance) or <= 42 (several), "
                "<= 1024 densities per mixture";
 
     // ---- native f32 layout ----

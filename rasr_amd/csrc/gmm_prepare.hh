@@ -123,6 +123,9 @@ struct PreparedFloat {
     // every mixture has an even number of tiles (pad tiles repeat the mixture's first row)
     uint32_t              splitKeyBits = 0;
     uint32_t              splitRows    = 16;  // tile height: 16 (16x16x32 MFMA, tile pairs) or 32 (32x32x16)
+    // several covariances on the split kernels (gmm_prepare.cc, the covariance-free expansion): the frame operand
+    // is [y^2, y] about the centre (prepareFramesSplitCov), dimScale has 2 D entries, K = 6 D + 4
+    bool                  splitCov     = false;
 };
 
 

@@ -166,14 +166,33 @@ def write_mixture_set(path: str, ms: MixtureSet, precision: int = 6) -> None:
 
 
 def synthetic_mixture_set(n_mixtures: int, densities_per_mixture, dimension: int, seed: int = 1234,
-                          n_covariances: int = 1, weights: str = "uniform") -> MixtureSet:
+                          n_covariances: int = 1, weights: str = "uniform", tying: str | None = None) -> MixtureSet:
     """SURVEY.md section 8(d) synthetic model.
 
     pooled variance  s2_k = 0.5 + |N(0,1)|;  means ~ N(0,1);  one mean per density;
     weights: "uniform" -> log(1/K_m);  "random" -> normalized Dirichlet(1) draws.
     densities_per_mixture: int, or a sequence of per-mixture counts (ragged models).
     n_covariances > 1 assigns every density a random covariance (untied variant).
+    tying (RASR's covariance-tying, src/Mm/Module.cc:54-58, 127-136) overrides n_covariances:
+    "pooled" one covariance, "mixture-specific" one per mixture, "none" one per density.
     """
+    if tying is not None:
+        if tying not in ("pooled", "mixture-specific", "none"):
+            raise ValueError(tying)
+        counts = (np.full(n_mixtures, int(densities_per_mixture), dtype=np.int64) if np.isscalar(densities_per_mixture)
+                  else np.asarray(densities_per_mixture, dtype=np.int64))
+        base = synthetic_mixture_set(n_mixtures, counts, dimension, seed, 1, weights)
+        if tying == "pooled":
+            return base
+        n = int(counts.sum())
+        c = n_mixtures if tying == "mixture-specific" else n
+        rng = np.random.Generator(np.random.PCG64(seed + 7))
+        var = (0.5 + np.abs(rng.standard_normal((max(c, 1), dimension), dtype=np.float32))).astype(np.float32)
+        dcov = (np.repeat(np.arange(n_mixtures, dtype=np.uint32), counts) if tying == "mixture-specific"
+                else np.arange(n, dtype=np.uint32))
+        return MixtureSet(means=base.means, variances=var, density_mean=base.density_mean, density_covariance=dcov,
+                          mixture_offsets=base.mixture_offsets, mixture_densities=base.mixture_densities,
+                          mixture_log_weights=base.mixture_log_weights)
     rng = np.random.Generator(np.random.PCG64(seed))
     if np.isscalar(densities_per_mixture):
         counts = np.full(n_mixtures, int(densities_per_mixture), dtype=np.int64)

@@ -8,7 +8,7 @@
 #   prof    : rocprofv3 --kernel-trace --stats over bench.py (BENCH_ARGS appended)
 #   ab-MODE : scripts/ab_bench.py --mode MODE over AB_LIBS (default: the variant libraries), AB_ARGS appended
 #   pmc-MODE: scripts/profile_pmc.sh MODE (one rocprofv3 --pmc pass per counter group, gpurun_out/pmc_MODE)
-#   line-X  : one other bench line, timed alone (X: sum sums d45 d45s pint pfloat nn ragged)
+#   line-X  : one other bench line, timed alone (X: sum sums d45 d45s pint pfloat nn ragged covm covn covms covsum)
 #   rehearse: the N > 1 bench flow on this one GPU (2 ranks on device 0, gloo in place of RCCL): headline, the
 #             fenced density-sharded / C-ABI children, the line
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -40,7 +40,10 @@ for s in ${STEPS:-pytest smoke}; do
       case ${s#line-} in
         sum) A="--mode sum" ;; sums) A="--mode sum --no-best" ;; d45) A="--dim 45" ;;
         d45s) A="--dim 45 --mode simd-scores" ;; pint) A="--mode presel-int" ;; pfloat) A="--mode presel-float" ;;
-        nn) A="--mode nn" ;; ragged) A="--ragged" ;; *) echo "unknown line $s"; exit 2 ;;
+        nn) A="--mode nn" ;; ragged) A="--ragged" ;;
+        covm) A="--tying mixture-specific" ;; covn) A="--tying none" ;; covms) A="--tying mixture-specific --mode simd" ;;
+        covsum) A="--tying none --mode sum" ;;
+        *) echo "unknown line $s"; exit 2 ;;
       esac
       step "$s" 300 python bench.py $A $B ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -148,7 +148,10 @@ def test_float_kernel_selection(gpu):
     assert ra.Scorer(_model(10, 4, 39, 1, "random"), "diagonal-maximum", split_tile32=True).main_kernel() == "scoreSplit32"
     assert ra.Scorer(_model(4, 600, 45, 1, "random"), "diagonal-maximum").main_kernel() == "scoreSplit"
     assert ra.Scorer(_model(10, 4, 60, 1, "random"), "diagonal-maximum", split_tile32=True).main_kernel() == "scoreSplit"
-    assert ra.Scorer(_model(10, 4, 39, 3, "random"), "diagonal-maximum").main_kernel() == "scoreF32"
+    # several covariances: the covariance-free split layout (K = 6 D + 4: 8 K steps at D = 39, the pair kernel)
+    assert ra.Scorer(_model(10, 4, 39, 3, "random"), "diagonal-maximum").main_kernel() == "scoreSplit"
+    assert ra.Scorer(_model(10, 4, 16, 3, "random"), "diagonal-maximum").main_kernel() == "scoreSplitWide"
+    assert ra.Scorer(_model(10, 4, 45, 3, "random"), "diagonal-maximum").main_kernel() == "scoreF32"  # 6D+4 > 256
     assert ra.Scorer(_model(10, 4, 39, 1, "random"), "diagonal-maximum", native_f32=True).main_kernel() == "scoreF32"
     assert ra.Scorer(_model(10, 4, 90, 1, "random"), "diagonal-maximum").main_kernel() == "scoreF32"  # 3D+7 > 256
 
@@ -225,12 +228,14 @@ def test_float_offset_narrow_gaussians(gpu, kopts, dim):
 
 
 def test_float_offset_narrow_gaussians_multi_covariance(gpu):
-    """Several covariances (scoreF32 with ||x'||^2 folded into K) on the offset, narrow model."""
+    """Several covariances on the offset, narrow model: the covariance-free split layout (D = 39) and scoreF32
+    (||x'||^2 folded into K, native_f32)."""
     ms = _offset_model(40, 12, 39, c=3)
     frames = _frames_near(ms, 300, seed=44)
     ref_s, ref_b = oracle.OracleFloat(ms).score(frames, n_threads=8)
-    s, b = _gpu_scores(ms, frames, "diagonal-maximum")
-    _check_float(s, b, ref_s, ref_b, ms, frames, None)
+    for opts in ({}, {"native_f32": True}):
+        s, b = _gpu_scores(ms, frames, "diagonal-maximum", **opts)
+        _check_float(s, b, ref_s, ref_b, ms, frames, None)
 
 
 def _edge_model():
