@@ -476,8 +476,8 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
         loadTile(T0 + 2 * j + 1, R[j][1], C[j][1]);
     }
 
-    // scores only (no best density, no preselection mask): keys are the values' own bits, nothing masked
-    const uint32_t kmask = (BEST || PRESEL) ? (1u << a.tileBits) - 1u : 0u;
+    // scores only (no best density; preselection-batch-float is a batch type): keys are the values' own bits
+    const uint32_t kmask = BEST ? (1u << a.tileBits) - 1u : 0u;
     // the value mask lives in a VGPR so that (bits & mask) | tag is ONE v_and_or_b32 with the tag in an
     // SGPR (gfx950 VOP3 reads at most one SGPR)
     uint32_t vmask = ~kmask;
@@ -527,13 +527,12 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
                 const uint32_t ka = (__float_as_uint(acc[0][cb][r]) & vmask) | tagA[r];
                 const uint32_t kb = (__float_as_uint(acc[1][cb][r]) & vmask) | tagB[r];
                 if constexpr (PRESEL) {
-                    // tag | sign-extended mask byte (one v_or_b32_sdwa), made opaque so that the key stays
-                    // one v_and_or_b32 (else the three ORs fold into v_or3 beside a separate v_and + v_bfe)
-                    uint32_t ca = tagA[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[0][cb / 4][r] >> (8 * (cb % 4)))));
-                    uint32_t cc = tagB[r] | static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[1][cb / 4][r] >> (8 * (cb % 4)))));
-                    asm("" : "+v"(ca), "+v"(cc));
-                    best[cb][r] = umin3(best[cb][r], (__float_as_uint(acc[0][cb][r]) & vmask) | ca,
-                                        (__float_as_uint(acc[1][cb][r]) & vmask) | cc);
+                    // preselection-batch-float has no best density: the key is the value's own bits OR the
+                    // sign-extended mask byte (one v_or_b32_sdwa per value; a deselected density becomes all ones,
+                    // above every value; round 5 carried the tile tag too: 2 VALU per value)
+                    const uint32_t ca = static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[0][cb / 4][r] >> (8 * (cb % 4)))));
+                    const uint32_t cc = static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(TT[1][cb / 4][r] >> (8 * (cb % 4)))));
+                    best[cb][r] = umin3(best[cb][r], __float_as_uint(acc[0][cb][r]) | ca, __float_as_uint(acc[1][cb][r]) | cc);
                 }
                 else if constexpr (BEST) {
                     best[cb][r] = umin3(best[cb][r], ka, kb);
@@ -658,10 +657,10 @@ __global__ __launch_bounds__(PRESEL ? kSplitFramesPerBlock / splitPreselNF(KS) *
 #define GMM_SPLIT_WIDE_PF 3  // tiles in flight
 #endif
 #ifndef GMM_SPLIT_WIDE_IL
-#define GMM_SPLIT_WIDE_IL 48  // MFMAs of a step interleaved 1 : 2 with the epilogue's VALU (at 16 blocks)
+#define GMM_SPLIT_WIDE_IL 64  // MFMAs of a step interleaved 1 : 2 with the epilogue VALU (at 16 blocks; 64 with one slot: -0.5 %, profiles/r06/s5)
 #endif
 #ifndef GMM_SPLIT_WIDE_SLOTS
-#define GMM_SPLIT_WIDE_SLOTS 2  // running minima per column block (1: the two min3 of a block chained)
+#define GMM_SPLIT_WIDE_SLOTS 1  // running minima per column block (1: the two min3 of a block chained; -1.3 %, profiles/r06/s5)
 #endif
 
 template <int KS, bool BEST>
