@@ -901,6 +901,12 @@ __global__ __launch_bounds__(64 * W, (KS == 1 && !PRESEL && GMM_I8_WAVES && W ==
 #ifndef GMM_I8_PRESEL_CPF
 #define GMM_I8_PRESEL_CPF 1  // preselection: the rows' cluster offsets read one tile ahead with the operands
 #endif
+#ifndef GMM_I8_PRESEL_SEG
+// preselection-batch-int: tiles per LDS segment, one workgroup barrier per segment (8: -3.9 % against 4; 16 +4.4 %, the
+// LDS then allows two waves per SIMD; profiles/r06/s6).  A lagged masked epilogue (the score-only step's pipeline, lag
+// 1 / 2 / 3) measured +6 / +17 / +17 % (profiles/r06/s7)
+#define GMM_I8_PRESEL_SEG 8
+#endif
 #ifndef GMM_I8_PRESEL_WAVES
 #define GMM_I8_PRESEL_WAVES 3  // preselection: waves per SIMD the register allocation must allow
 #endif
@@ -1337,7 +1343,7 @@ static void launchI8T(const I8Args& a, uint32_t grid, hipStream_t s) {
     if constexpr (!MULTI) {
         if (a.presel && a.scoreOnly == 2) {  // preselection-batch-int on the slot layout (3 waves per SIMD: registers)
             if constexpr (KS == 1 && kI8PreselNF == 8) {
-                constexpr int      kSeg = 4;
+                constexpr int      kSeg = GMM_I8_PRESEL_SEG;
                 constexpr uint32_t kRing = 2 * kSeg * (1024 + 64 + 64) + 64;
                 const uint32_t     lds   = kRing + 4u * (a.nClusters * 16u + 16u) * 2u;
                 constexpr int      kMax  = static_cast<int>(kRing + 4u * (256u * 16u + 16u) * 2u);
