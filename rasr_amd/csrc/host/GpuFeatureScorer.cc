@@ -383,6 +383,7 @@ std::unique_ptr<GpuBatchFeatureScorer> GpuBatchFeatureScorer::create(const Mixtu
     }
     s->cached_.assign(b, 0);
     s->generation_.assign(b, 0);
+    s->sparsePos_.assign(b, 0);
     s->bestCached_.assign(b, 0);
     s->bestCall_.assign(b, 0);
     s->inflight_.assign(b, 0);
@@ -405,6 +406,7 @@ void GpuBatchFeatureScorer::reset() const {
     for (uint32_t& g : generation_)
         ++g;
     sparse_.clear();  // every position's frame is gone
+    std::fill(sparsePos_.begin(), sparsePos_.end(), 0);
     pendingCount_   = 0;
     currentFeature_ = 0;
     buffered_       = 0;
@@ -418,8 +420,11 @@ void GpuBatchFeatureScorer::setFeature(size_t pos, const FeatureVector& f) const
     ++generation_[pos];
     // the position's single-pair answers belonged to its previous frame (once every position took a new frame
     // the map is empty and bestDensity() skips the lookup)
-    for (auto i = sparse_.begin(); i != sparse_.end();)
-        i = (i->first >> 32) == pos ? sparse_.erase(i) : std::next(i);
+    if (sparsePos_[pos]) {
+        for (auto i = sparse_.begin(); i != sparse_.end();)
+            i = (i->first >> 32) == pos ? sparse_.erase(i) : std::next(i);
+        sparsePos_[pos] = 0;
+    }
     if (!prefetchChunk_)
         return;
     // the new frame joins the pending run (it is the newest buffered position)
@@ -554,9 +559,9 @@ const DensityInMixture* GpuBatchFeatureScorer::bestRow(uint32_t featureIndex, ui
 }
 
 bool GpuBatchFeatureScorer::sparseAnswer(uint32_t featureIndex, EmissionIndex e, DensityInMixture* v) const {
-    if (sparse_.empty())
+    const uint32_t p = featureIndex % bufferSize_;
+    if (!sparsePos_[p])  // (one test per call: a full dump asks every emission's best density)
         return false;
-    const uint32_t p  = featureIndex % bufferSize_;
     const auto     it = sparse_.find((static_cast<uint64_t>(p) << 32) | e);
     if (it == sparse_.end() || it->second.first != generation_[p])
         return false;
@@ -588,15 +593,14 @@ DensityInMixture GpuBatchFeatureScorer::getBestDensity(EmissionIndex e, uint32_t
     if (call != sparseCall_) {
         sparseCall_  = call;
         sparseAsked_ = 0;
-        for (auto i = sparse_.begin(); i != sparse_.end();)  // answers of frames no longer buffered
-            i = i->second.first == generation_[i->first >> 32] ? std::next(i) : sparse_.erase(i);
     }
     if (sparseAsked_ < kSparseMax) {
         uint32_t pos = p, v = 0;
         if (gmm_best_density_pairs(handle_, call, &pos, &e, 1, &v) == GMM_OK) {
             ++sparseAsked_;
             ++bestPairs_;
-            sparse_[key] = {generation_[p], v};
+            if (sparse_.insert_or_assign(key, std::make_pair(generation_[p], v)).second)
+                ++sparsePos_[p];
             return v;
         }
     }

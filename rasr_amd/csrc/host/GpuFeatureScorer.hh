@@ -301,6 +301,7 @@ private:
     // answer for that frame (CachedAssigningContextScorer memoizes, AssigningFeatureScorer.hh:110-121), even after
     // the position's whole table was fetched in the keyed scorer's arithmetic
     mutable std::unordered_map<uint64_t, std::pair<uint32_t, DensityInMixture>> sparse_;
+    mutable std::vector<uint16_t> sparsePos_;  // [bufferSize] entries of sparse_ per position (0: no lookup)
     mutable int32_t           currentFeature_ = 0;
     mutable int32_t           buffered_       = 0;
     mutable uint32_t          launches_       = 0, bestFetches_ = 0, bestPairs_ = 0;

@@ -116,6 +116,9 @@ def test_diagonal_sum_edges(gpu):
 
 @pytest.mark.gpu
 def test_diagonal_sum_needs_split_kernel(gpu):
+    # several covariances: the covariance-free split layout up to dimension 42 (K = 6 D + 4 <= 256), refused beyond
     ms = ra.synthetic_mixture_set(10, 4, 39, seed=1, n_covariances=3)
-    with pytest.raises(ra.GmmError):
+    assert ra.Scorer(ms, "diagonal-sum").main_kernel() == "scoreSplitSum"
+    ms = ra.synthetic_mixture_set(10, 4, 45, seed=1, n_covariances=3)
+    with pytest.raises(ra.GmmError, match="diagonal-sum"):
         ra.Scorer(ms, "diagonal-sum")
