@@ -1,31 +1,31 @@
 #!/usr/bin/env python3
-"""Per-kernel statistics from a rocprofv3 --kernel-trace database (rocpd sqlite, the default output format of
-rocprofv3 in this image), split by launch geometry so the headline launch size can be read off on its own:
-  rocpd_stats.py <run_results.db> [--csv OUT] [--top N] [--min-ms T]
-Columns: kernel, grid (threads), workgroup, launches, avg / min / max / total duration (ms).  --min-ms keeps launches
-of at least T ms (bench.py's 32768-frame launches share their grid with its 4096-frame small-batch launches)."""
+"""Per-kernel statistics from a rocprofv3 --kernel-trace database (rocpd SQLite, the ROCm 7 default output):
+kernel, grid, workgroup, launches, avg/min/max/total ms -- the columns of profiles/r05/*/kernel_stats.csv.
+usage: rocpd_stats.py <run_results.db> [--min-ms X] > kernel_stats.csv"""
 import argparse
 import csv
 import sqlite3
 import sys
+from collections import defaultdict
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--csv", default=None)
-    ap.add_argument("--top", type=int, default=25)
-    ap.add_argument("--min-ms", type=float, default=0.0)
+    ap.add_argument("--min-ms", type=float, default=0.0, help="only dispatches at least this long (e.g. 3 for 32768-frame launches)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = c.execute("select name, grid_x, workgroup_x, count(*), avg(end - start), min(end - start), "
-                     "max(end - start), sum(end - start) from kernels where end - start >= ? group by name, grid_x, workgroup_x "
-                     "order by sum(end - start) desc", (int(a.min_ms * 1e6),)).fetchall()
-    out = [["kernel", "grid", "workgroup", "launches", "avg_ms", "min_ms", "max_ms", "total_ms"]]
-    for n, g, w, k, av, mn, mx, tot in rows[: a.top]:
-        out.append([n, g, w, k, f"{av / 1e6:.4f}", f"{mn / 1e6:.4f}", f"{mx / 1e6:.4f}", f"{tot / 1e6:.2f}"])
-    wr = csv.writer(open(a.csv, "w", newline="") if a.csv else sys.stdout)
-    wr.writerows(out)
+    names = {r[0]: r[1] for r in c.execute("select id, kernel_name from rocpd_info_kernel_symbol")}
+    groups = defaultdict(list)
+    for kid, start, end, gx, wx in c.execute(
+            "select kernel_id, start, end, grid_size_x, workgroup_size_x from rocpd_kernel_dispatch"):
+        ms = (end - start) * 1e-6
+        if ms >= a.min_ms:
+            groups[(names.get(kid, str(kid)), gx, wx)].append(ms)
+    w = csv.writer(sys.stdout)
+    w.writerow(["kernel", "grid", "workgroup", "launches", "avg_ms", "min_ms", "max_ms", "total_ms"])
+    for (name, gx, wx), v in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
+        w.writerow([name, gx, wx, len(v), f"{sum(v) / len(v):.4f}", f"{min(v):.4f}", f"{max(v):.4f}", f"{sum(v):.2f}"])
 
 
 if __name__ == "__main__":
