@@ -123,3 +123,17 @@ def test_simd_untied_small_calls_bit_exact_and_refusal(gpu):
     big = ra.synthetic_mixture_set(2000, 100, 39, seed=34, tying="none")  # 200k covariances
     with pytest.raises(ra.GmmError, match="covariances"):
         ra.Scorer(big, "SIMD-diagonal-maximum", max_frames=1 << 20)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tying", TYINGS)
+def test_float_tying_density_sharded(gpu, tying):
+    """gmm_scorer_create_sharded (three parts on device 0, mixtures split between parts) on a model without a pooled
+    covariance: every part on the covariance-free layout, the split mixtures combined by the key exchange."""
+    counts = ra.ragged_counts(30, 30 * 14, low=1, high=40, seed=35)
+    ms = ra.synthetic_mixture_set(30, counts, 39, seed=35, weights="random", tying=tying)
+    frames = ra.synthetic_frames(100, 39, seed=36)
+    ref_s, ref_b = oracle.OracleFloat(ms).score(frames, n_threads=8)
+    sc = ra.Scorer(ms, "diagonal-maximum", max_frames=128, devices=[0, 0, 0], exchange="copy")
+    s, b = sc.score_host(frames)
+    _check_float(s, b, ref_s, ref_b, ms, frames, None)
