@@ -137,3 +137,31 @@ def test_float_tying_density_sharded(gpu, tying):
     sc = ra.Scorer(ms, "diagonal-maximum", max_frames=128, devices=[0, 0, 0], exchange="copy")
     s, b = sc.score_host(frames)
     _check_float(s, b, ref_s, ref_b, ms, frames, None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,kernel", [(42, "scoreSplit"), (43, "scoreF32"), (20, "scoreSplitWide"), (21, "scoreSplit")])
+def test_float_tying_dimension_boundaries(gpu, d, kernel):
+    """K = 6 D + 4: the covariance-free layout up to D = 42 (8 K steps; 4 for the 256-frame kernel at D <= 20), the
+    f32-MFMA kernel beyond -- the same scores either way."""
+    ms = ra.synthetic_mixture_set(12, 9, d, seed=40 + d, weights="random", tying="mixture-specific")
+    frames = ra.synthetic_frames(70, d, seed=41)
+    sc = ra.Scorer(ms, "diagonal-maximum", max_frames=70)
+    assert sc.main_kernel() == kernel
+    s, b = sc.score_host(frames)
+    ref_s, ref_b = oracle.OracleFloat(ms).score(frames, n_threads=8)
+    _check_float(s, b, ref_s, ref_b, ms, frames, None)
+
+
+@pytest.mark.gpu
+def test_sum_tying_edges(gpu):
+    """diagonal-sum without tying: an empty mixture (+inf, no density), one-density mixtures (the sum is the
+    maximum's score), mixtures past 64 densities, and frames far out."""
+    counts = [0, 1, 3, 70, 1, 20]
+    ms = ra.synthetic_mixture_set(6, counts, 39, seed=42, weights="random", tying="none")
+    frames = ra.synthetic_frames(40, 39, seed=43)
+    frames[:4] *= 30.0
+    ref_s, ref_b = oracle.OracleFloatSum(ms).score(frames, n_threads=8)
+    s, b = ra.Scorer(ms, "diagonal-sum", max_frames=40).score_host(frames)
+    assert np.isinf(s[0]).all() and (b[0] == 0xFFFFFFFF).all()
+    _check_float(s[1:], b[1:], ref_s[1:], ref_b[1:], ms, frames, None, mixture_offset=1)
