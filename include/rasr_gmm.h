@@ -43,7 +43,8 @@ typedef enum {
     GMM_DIAGONAL_SUM                 = 12 /* diagonalSum: GaussDiagonalSumFeatureScorer
                                              (GaussDiagonalMaximumFeatureScorer.cc:221-298), no
                                              registration string in the reference factory; here
-                                             "diagonal-sum".  One covariance, split-f16 kernel only. */
+                                             "diagonal-sum".  Split-f16 kernels only: one covariance
+                                             (dimension <= 83) or several (dimension <= 42). */
 } gmm_scorer_type;
 
 /* In-memory Mm::MixtureSet (src/Mm/MixtureSet.hh:140-212).  Replaces what the
@@ -87,9 +88,11 @@ typedef struct {
     const char* cache_archive;
 } gmm_scorer_config;
 
-/* Float types (diagonal-maximum, batch-float) with one covariance run on the f16
- * matrix cores with every f32 operand split into two f16 pieces (f32 accuracy
- * class); this flag selects the f32-MFMA kernel instead. */
+/* Float types (diagonal-maximum, batch-float, diagonal-sum) run on the f16 matrix cores with every f32 operand
+ * split into two f16 pieces (f32 accuracy class).  Several covariances (covariance-tying none or
+ * mixture-specific, diagonal-maximum / diagonal-sum) take the covariance-free layout: one frame operand
+ * [(x - c)^2, (x - c)] for every covariance, K = 6 dimension + 4, dimension <= 42; beyond that the f32-MFMA kernel
+ * with per-covariance frame operands.  This flag selects the f32-MFMA kernel always. */
 #define GMM_FLAG_NATIVE_F32 1u
 /* Tile height of the split-f16 kernel.  By default 32-density tiles (v_mfma_f32_32x32x16_f16, K in
  * steps of 16) are used where they save more than 5 % of K over 16-density tiles (v_mfma_f32_16x16x32_f16,
@@ -126,7 +129,10 @@ void gmm_default_config(gmm_scorer_config* cfg);
 /* Prepare the model on the host exactly as the reference scorer's init() does
  * (quantization scale, 1/sqrt(var), prepared means, constant weights) and
  * upload it to `device`.  Replaces the FeatureScorerFactory::createInstance
- * call (src/Mm/FeatureScorerFactory.hh:114-122) for the selected type. */
+ * call (src/Mm/FeatureScorerFactory.hh:114-122) for the selected type.
+ * SIMD-diagonal-maximum with several covariances quantizes each frame per covariance (SimdFeatureScorer.cc:22-35)
+ * into a covariances x max_frames x 64 B table: GMM_ERR_UNSUPPORTED, the size in gmm_last_error(), when that table
+ * exceeds three quarters of the device's free memory. */
 int gmm_scorer_create(const gmm_mixture_set* mixture_set, gmm_scorer_type type,
                       const gmm_scorer_config* config, int device, gmm_scorer** out);
 int gmm_scorer_destroy(gmm_scorer* scorer);
