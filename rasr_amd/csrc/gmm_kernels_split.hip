@@ -1428,7 +1428,7 @@ __device__ __forceinline__ void emitMixtureSplit32Sum(const SplitArgs& a, const 
 }
 
 #ifndef GMM_SPLIT32_SUM_IL
-#define GMM_SPLIT32_SUM_IL 10  // VALU per MFMA in the interleave of a step (the epilogue's ~316 VALU beside 32 MFMAs)
+#define GMM_SPLIT32_SUM_IL 6  // VALU per MFMA in the interleave of a step (6: -1.8 % against 10, 13 +2 %; profiles/r06/s14, s15)
 #endif
 
 template <int KS, bool BEST>
