@@ -877,6 +877,9 @@ __device__ __forceinline__ void emitMixtureSplit32(const SplitArgs& a, const uin
     }
 }
 
+#ifndef GMM_SPLIT32_IL
+#define GMM_SPLIT32_IL 3  // scoreSplit32: VALU per MFMA in a step's interleave
+#endif
 #ifndef GMM_SPLIT32_NB
 #define GMM_SPLIT32_NB 4  // 32-frame column blocks per wave of scoreSplit32 (4: 128 frames, B in the AGPRs; 2: 64)
 #endif
@@ -1003,14 +1006,14 @@ __global__ __launch_bounds__(64 * (kSplitFramesPerBlock / (32 * GMM_SPLIT32_NB))
             advance(tNext);
         }
     };
-    // MFMAs of the tile in A into cur beside the epilogue of tile tPrev (in prev), 1 MFMA : 3 VALU
+    // MFMAs of the tile in A into cur beside the epilogue of tile tPrev (in prev), 1 MFMA : GMM_SPLIT32_IL VALU
     const auto step = [&](const f16x8(&A)[KS], f32x16(&cur)[NB], const f32x16(&prev)[NB], uint32_t tPrev) {
         chain(A, cur);
         epilogue(prev, tPrev - tBeg);
 #pragma unroll
         for (int i = 0; i < NB * KS; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, GMM_SPLIT32_IL, 0);  // VALU
         }
     };
 
