@@ -1177,12 +1177,11 @@ __global__ __launch_bounds__(64 * W, W == 4 ? (PRESEL ? GMM_I8_PRESEL_WAVES : (N
             i32x4 C = Cpf;
             if constexpr (!GMM_I8_PRESEL_CPF)
                 C = *reinterpret_cast<const i32x4*>(cptr);
-            // The LUT reads are inline asm: a compiler-visible 64-bit LDS read at a loaded address makes the
-            // waitcnt pass drain the LDS-DMA queue (s_waitcnt vmcnt(0)) at every step, since it cannot tell the
-            // read from the ring the DMA fills; their lgkmcnt wait is explicit, before the epilogues
-            // (the 64-bit LUT read makes the waitcnt pass wait for the LDS-DMA queue, s_waitcnt vmcnt(0): by then
-            // the next segment, issued a segment ahead, has landed; two 32-bit reads from split tables avoid the
-            // wait but measured 11 % slower, profiles/r05/s9)
+            // The 64-bit LUT read at a loaded address makes the waitcnt pass drain the LDS-DMA queue (s_waitcnt
+            // vmcnt(0)) at every step, since it cannot tell the read from the ring the DMA fills; by then the next
+            // segment, issued a segment ahead, has landed.  Two 32-bit reads from split tables avoid the wait but
+            // measured 11 % slower (profiles/r05/s9), a conflict-free 16-entry nibble LUT 3.5 % slower
+            // (profiles/r06/s24), these reads one step ahead flat (profiles/r06/s22)
             prefetch();
             MaskW T[4];
 #pragma unroll
